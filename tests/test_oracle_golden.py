@@ -1,0 +1,155 @@
+"""Pin the CPU oracle against the golden fixtures generated from the reference.
+
+The oracle restates the reference's torch-CPU op sequence, so these checks are
+BIT-EXACT (``torch.equal``) unless a comment says otherwise.  CPU only.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import mppi_oracle as O
+
+
+def _eq(a, b):
+    a = torch.as_tensor(np.asarray(a))
+    b = torch.as_tensor(np.asarray(b))
+    assert a.dtype == b.dtype, (a.dtype, b.dtype)
+    assert torch.equal(a, b), f"max|d|={(a.double() - b.double()).abs().max().item()}"
+
+
+@pytest.fixture(autouse=True)
+def _threads():
+    n = torch.get_num_threads()
+    torch.set_num_threads(1)
+    yield
+    torch.set_num_threads(n)
+
+
+def test_origin_matrices_match_reference(kinova_chain):
+    g = load_golden("fk_known_answer.npz")
+    for j, ref in zip(kinova_chain, g["origins"]):
+        _eq(O.origin_matrix(j.xyz, j.rpy).numpy(), ref)
+
+
+@pytest.mark.parametrize("b", range(4))
+def test_fk_batched_fp32_and_fp64(kinova_chain, b):
+    g = load_golden("fk_known_answer.npz")
+    q32 = torch.from_numpy(g["q32"])
+    base = torch.from_numpy(g["bases"][b])
+    _eq(O.ee_world(kinova_chain, q32, base).numpy(), g[f"ee32_b{b}"])
+    _eq(O.ee_world(kinova_chain, q32.double(), base.double()).numpy(), g[f"ee64_b{b}"])
+
+
+@pytest.mark.parametrize("b", range(4))
+def test_fk_single_host_path(kinova_chain, b):
+    g = load_golden("fk_known_answer.npz")
+    q32 = torch.from_numpy(g["q32"])
+    base = torch.from_numpy(g["bases"][b])
+    got = np.stack([O.ee_world_single(kinova_chain, q32[0, j], base).numpy() for j in range(4)])
+    _eq(got, g[f"eecpu_b{b}"])
+
+
+def test_rotation_utils():
+    g = load_golden("rotations.npz")
+    _eq(O.quat_xyzw_matrix(torch.from_numpy(g["quat"])).numpy(), g["quat_R"])
+    _eq(O.euler_zyx(torch.from_numpy(g["mats"])).numpy(), g["euler"])
+    _eq(O.quat_xyzw_matrix(torch.tensor([-0.5, -0.5, 0.5, -0.5])).numpy(), g["target_R"])
+
+
+def test_savgol():
+    g = load_golden("savgol.npz")
+    for key in [k for k in g if k.startswith("x_")]:
+        H, A, W, P = map(int, key.split("_")[1:])
+        _eq(O.savgol(torch.from_numpy(g[key]), W, P).numpy(), g["y" + key[1:]])
+    # coefficients recovered from the reference's impulse response
+    for key in [k for k in g if k.startswith("coef_")]:
+        W, P = map(int, key.split("_")[1:])
+        np.testing.assert_allclose(O.savgol_coefficients(W, P).numpy(), g[key], rtol=0, atol=1e-7)
+
+
+def test_savgol_rejects_short_sequences():
+    with pytest.raises(ValueError):
+        O.savgol(torch.zeros(4, 2), 9, 2)
+
+
+@pytest.mark.parametrize("name", ["drone_k128_h20.npz", "drone_k256_h32.npz"])
+def test_drone_steps(name):
+    g = load_golden(name)
+    H = int(g["H"])
+    for s in range(int(g["steps"])):
+        r = O.drone_step(g[f"s{s}_x_in"], g[f"s{s}_v_in"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
+                         torch.from_numpy(g[f"s{s}_noise"]), g["target"])
+        for k in ("traj", "S", "w", "w_eps_raw", "w_eps", "u_prev_out", "x_out", "v_out"):
+            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+        assert r["u_prev_out"].shape == (H, 3)
+
+
+def test_drone_noise_reproduces_reference_randn():
+    """torch.manual_seed(seed) + randn + Sigma reproduces the recorded noise."""
+    g = load_golden("drone_k128_h20.npz")
+    torch.manual_seed(100)
+    eps = O.draw_noise(128, 20, torch.from_numpy(g["sigma"]))
+    _eq(eps.numpy(), g["s0_noise"])
+
+
+@pytest.mark.parametrize("name", ["arm_k32_h32_f32.npz", "arm_k32_h32_f64.npz", "arm_k100_h32_f64.npz"])
+def test_arm_steps(kinova_chain, name):
+    g = load_golden(name)
+    f64 = bool(g["state_f64"])
+    for s in range(int(g["steps"])):
+        r = O.arm_step(kinova_chain, g["q_full"], g["v_full"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
+                       torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"], f64=f64)
+        for k in ("v", "q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out"):
+            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+        _eq(r["qdes"], g[f"s{s}_qdes"])
+        _eq(r["vdes"], g[f"s{s}_vdes"])
+        assert r["reach"] == bool(g[f"s{s}_reach"])
+
+
+def test_arm_noise_reproduces_reference_randn():
+    g = load_golden("arm_k32_h32_f32.npz")
+    torch.manual_seed(300)
+    _eq(O.draw_noise(32, 32, torch.eye(7) * 0.1).numpy(), g["s0_noise"])
+
+
+def test_wholebody_steps(kinova_chain):
+    g = load_golden("wholebody_k32_h64.npz")
+    _eq(O.base_rpy_from_quat(g["base_quat"]).numpy(), g["base_rpy"])
+    for s in range(int(g["steps"])):
+        r = O.wholebody_step(kinova_chain, g[f"s{s}_x_in"], g[f"s{s}_vx_in"], g[f"s{s}_q_in"],
+                             g[f"s{s}_qd_in"], g["base_rpy"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
+                             torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"])
+        for k in ("q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out",
+                  "x_out", "v_out", "qdes", "vdes"):
+            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+
+
+def test_shard_combine_equals_global_softmin():
+    """The §8e combine (any shard split) equals the global softmin-weighted sum."""
+    g = load_golden("drone_k256_h32.npz")
+    S = torch.from_numpy(g["s1_S"])
+    eps = torch.from_numpy(g["s1_noise"])
+    ref = torch.from_numpy(g["s1_w_eps_raw"]).double()
+    for G in (1, 2, 4, 8):
+        parts = [O.shard_partial(S[i::G], eps[i::G], 0.1) for i in range(G)]
+        got = O.combine_partials(parts, 0.1)
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_philox_known_answer():
+    """Random123 known-answer vectors for philox4x32-10."""
+    out = O.philox4x32_10(0, 0, 0, 0, 0, 0)
+    assert [int(x) for x in out] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    out = O.philox4x32_10(0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff)
+    assert [int(x) for x in out] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    out = O.philox4x32_10(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0)
+    assert [int(x) for x in out] == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_philox_normals_moments():
+    raw, z = O.philox_normals(1234, 0, 0, np.arange(4096), 32, 4)
+    z = z.astype(np.float64).ravel()
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    from scipy import stats
+    assert stats.kstest(z[:20000], "norm").pvalue > 1e-3
