@@ -1,0 +1,223 @@
+/*
+ * mppi_hip.h -- C-ABI of the MI355X-native MPPI rollout engine (libmppi_hip.so).
+ *
+ * Drop-in boundary for the mav_mppi control step.  The
+ * reference has no native FFI: its hot path is the Python methods below, and a
+ * host binding (ctypes, quadrotor_manipulator_mppi_amd/_capi.py) replaces the
+ * torch op sequence each entry point stands for:
+ *
+ *   mppi_create         <- MPPI.__init__            mppi_solver/mppi.py:28-93,
+ *                                                   mppi_solver/drone_mppi.py:8-37
+ *   mppi_set_state      <- MPPI.update_joint        mppi.py:196-200 (arm),
+ *                          MPPI.set_state           drone_mppi.py:179-183 (drone)
+ *   mppi_set_target     <- target_pose / target     mppi.py:70-72, drone_mppi.py:141
+ *   mppi_rollout        <- sampling + rollout + FK + cost + softmin partials
+ *                          mppi.py:129-143 / drone_mppi.py:142-156
+ *                          (standard_normal_noise.py:22-50, urdf_fk.py:79-108,
+ *                           urdfparser.py:122-163, pose_cost.py:24-63)
+ *   mppi_finalize       <- weighted noise + SavGol + control update
+ *                          mppi.py:144-158 / drone_mppi.py:157-169
+ *                          (mppi.py:173-193, svg_filter.py:13-90)
+ *   mppi_read_outputs   <- the (qdes, vdes) / (x, v) returned by
+ *                          compute_control_input (mppi.py:161-169 incl. the
+ *                          check_reach host FK at :95-120; drone_mppi.py:175)
+ *   mppi_step           <- MPPI.compute_control_input as one call
+ *   mppi_get_*          <- the reference's intermediate tensors (noise,
+ *                          q_samples/trajectory, S, weights, w_eps, u_prev),
+ *                          returned in the reference's own layouts
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Host pointers unless
+ * a name says d_ (device).  Every call returns mppi_status (0 = ok); on error
+ * mppi_last_error() returns a thread-local message.  Calls on one engine must be
+ * serialised by the caller (the Python wrapper holds a lock).
+ */
+#ifndef MPPI_HIP_H
+#define MPPI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPPI_ABI_VERSION 1
+#define MPPI_MAX_ACTION 16
+#define MPPI_MAX_JOINTS 16
+#define MPPI_MAX_HORIZON 256
+#define MPPI_MAX_SAVGOL 31
+
+typedef enum {
+    MPPI_OK = 0,
+    MPPI_ERR_INVALID_ARG = -1,
+    MPPI_ERR_HIP = -2,
+    MPPI_ERR_NONFINITE = -3,
+    MPPI_ERR_STATE = -4
+} mppi_status;
+
+/* Rollout models.  A = action dimension. */
+typedef enum {
+    MPPI_MODEL_DRONE = 0,     /* xyz double integrator, squared position cost      (A=3)  drone_mppi.py   */
+    MPPI_MODEL_ARM = 1,       /* joint double integrator + FK chain + pose cost    (A=nq) mppi.py         */
+    MPPI_MODEL_WHOLEBODY = 2  /* drone xyz + arm joints, mobile-base FK, pose cost (A=3+nq) SURVEY A16    */
+} mppi_model;
+
+typedef enum {
+    MPPI_NOISE_PHILOX = 0,    /* device counter-based Philox4x32-10 + Box-Muller (production)          */
+    MPPI_NOISE_INJECTED = 1   /* caller supplies eps (K,H,A) per step (parity: reference randn noise)  */
+} mppi_noise_mode;
+
+typedef enum { MPPI_JOINT_FIXED = 0, MPPI_JOINT_REVOLUTE = 1, MPPI_JOINT_PRISMATIC = 2 } mppi_joint_type;
+
+/* One entry of the active joint chain (urdfparser.py:133-161). xyz/rpy/axis as
+ * the URDF floats (rounded to fp32 like torch.tensor(jt.origin.xyz)). */
+typedef struct {
+    int32_t type;       /* mppi_joint_type                                   */
+    int32_t q_index;    /* index into the arm joint vector, -1 if not actuated */
+    float xyz[3];
+    float rpy[3];
+    float axis[3];      /* raw URDF axis; normalised like transformation_matrix.py:63-66 */
+    int32_t has_axis;   /* 0 -> (1,0,0) as urdfparser.py:140-143              */
+} mppi_joint;
+
+typedef struct {
+    int32_t model;            /* mppi_model                                                     */
+    int32_t n_vehicles;       /* V independent controllers batched in one launch (config C5)    */
+    int32_t n_samples;        /* K samples owned by THIS engine (one shard)                      */
+    int32_t n_horizon;        /* H                                                              */
+    int32_t n_action;         /* A (3 drone, nq arm, 3+nq whole-body)                           */
+    double dt;                /* 0.01 (mppi.py:42, drone_mppi.py:18); a Python float there       */
+    double lambda_;           /* 0.1  (mppi.py:75, drone_mppi.py:33)                             */
+    float sigma[MPPI_MAX_ACTION * MPPI_MAX_ACTION]; /* Sigma (A x A, row-major), eps = z^T Sigma */
+    /* cost weights: pose (stage pos, stage ori, terminal pos, terminal ori) = 50,30,40,30
+     * (cost_manager.py:25-28); drone uses w_stage_pos=100, w_term_pos=20 (drone_mppi.py:92,104) */
+    float w_stage_pos, w_stage_ori, w_term_pos, w_term_ori;
+    int32_t n_joints;
+    mppi_joint joints[MPPI_MAX_JOINTS];
+    int32_t savgol_window;    /* 5 drone, 9 arm (drone_mppi.py:160, mppi.py:149)                */
+    int32_t savgol_order;     /* 2                                                              */
+    int32_t noise_mode;       /* mppi_noise_mode                                                */
+    uint64_t seed;            /* Philox key                                                     */
+    int32_t device;           /* HIP device ordinal                                             */
+    int32_t shard_rank;       /* sample sharding: this engine owns global samples               */
+    int32_t shard_count;      /*   [rank*K, (rank+1)*K); partials exchanged by the caller       */
+    int32_t state_f64;        /* reproduce the reference's fp64 promotion of an fp64 arm state  */
+    int32_t store_trajectory; /* write the trajectory buffer (q / p and EE 3x4 per (k,t))       */
+    int32_t store_noise;      /* write eps (K,H,A) (debug / parity readback)                    */
+    int32_t check_reach;      /* host FK at qdes, L1 position error < reach_tol (mppi.py:95-120)*/
+    float reach_tol;          /* 0.005                                                          */
+    int32_t blocks_per_vehicle; /* rollout grid.x; 0 = auto                                     */
+    int32_t block_threads;      /* rollout block size (multiple of 64); 0 = auto                */
+} mppi_config;
+
+/* Per-vehicle statistics of the last finalised step. */
+typedef struct {
+    float rho;          /* min_k S_k                                        */
+    float eta;          /* sum_k exp(-(S_k - rho)/lambda)                   */
+    float ess;          /* effective sample size 1 / sum_k w_k^2            */
+    int32_t nonfinite;  /* 1 if rho/eta/u is not finite (reference propagates NaN) */
+    int32_t reach;      /* check_reach result (arm / whole-body)            */
+    int32_t _pad;
+} mppi_stats;
+
+typedef struct mppi_engine mppi_engine;
+
+int32_t mppi_abi_version(void);
+const char* mppi_last_error(void);
+/* sizeof(mppi_config), sizeof(mppi_joint), sizeof(mppi_stats): lets a binding check its layout. */
+void mppi_struct_sizes(int32_t* config, int32_t* joint, int32_t* stats);
+
+/* Reference defaults for a model (drone: K=1000 H=32 sigma=30I; arm: K=100 H=32
+ * sigma=0.1I, Kinova chain must still be filled in by the caller). */
+void mppi_config_default(mppi_config* cfg, int32_t model);
+
+/* Sizes of the packed host-side state / output rows for a config. */
+int32_t mppi_state_dim(const mppi_config* cfg);   /* doubles per vehicle  */
+int32_t mppi_output_dim(const mppi_config* cfg);  /* doubles per vehicle  */
+int32_t mppi_traj_channels(const mppi_config* cfg);
+
+mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out);
+void mppi_destroy(mppi_engine* e);
+
+/* Run on a caller stream (hipStream_t cast to void*); NULL = engine-owned stream. */
+mppi_status mppi_set_stream(mppi_engine* e, void* hip_stream);
+
+/* Goal per vehicle: position (3) and orientation quaternion xyzw (4; ignored by DRONE). */
+mppi_status mppi_set_target(mppi_engine* e, int32_t vehicle, const float* pos3, const float* quat_xyzw4);
+
+/* Warm start (V,H,A) -- reference attribute u_prev (mppi.py:58, drone_mppi.py:29). */
+mppi_status mppi_set_u_prev(mppi_engine* e, const float* u_prev);
+mppi_status mppi_get_u_prev(mppi_engine* e, float* u_prev);
+
+/* Measured state, packed per vehicle (doubles):
+ *   DRONE:     x(3) v(3)
+ *   ARM:       base xyz(3) quat xyzw(4) q(nq) qd(nq)        (q_full[:7]+q_full[7:], v_full[6:])
+ *   WHOLEBODY: base xyz(3) quat xyzw(4) q(nq) base vel(3) qd(nq)
+ * Async host->device (pinned staging) on the engine stream. */
+mppi_status mppi_set_state(mppi_engine* e, const double* state);
+
+/* Step counter used as the Philox counter word (device resident). */
+mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step);
+
+/* Split-phase step (async, stream ordered).  d_noise: device eps (V,K,H,A) in
+ * INJECTED mode, else NULL.  With shard_count > 1 bind an exchange buffer of
+ * shard_count*V*slot floats (zeroed and filled with this shard's slot by
+ * mppi_rollout); the caller sums it across shards (one all-reduce), then calls
+ * mppi_finalize. */
+mppi_status mppi_exchange_slot_floats(mppi_engine* e, int64_t* slot_floats);
+mppi_status mppi_bind_exchange(mppi_engine* e, float* d_exchange);
+mppi_status mppi_rollout(mppi_engine* e, const float* d_noise);
+mppi_status mppi_finalize(mppi_engine* e);
+
+/* Synchronise and copy the step's outputs: out (V, output_dim) doubles
+ *   DRONE: x_des(3) v_des(3);  ARM: qdes(nq) vdes(nq);  WHOLEBODY: x(3) v(3) qdes(nq) vdes(nq)
+ * u0 (V, A) floats and stats (V) may be NULL. */
+mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats);
+
+/* One whole control step: set_state, (upload host noise), rollout, finalize, read_outputs.
+ * h_noise: host eps (V,K,H,A) in INJECTED mode, else NULL.  Single-shard only. */
+mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out,
+                      float* u0, mppi_stats* stats);
+
+mppi_status mppi_synchronize(mppi_engine* e);
+
+/* Readback in the reference's layouts (synchronous):
+ *   costs    S (V,K)                         compute_all_cost()
+ *   weights  w (V,K)                         compute_weights()
+ *   noise    eps (V,K,H,A)                   sampling()            [store_noise]
+ *   traj     (V,K,H,C) C = traj_channels    DRONE p(3) / ARM q(nq)+EE(16) / WB p(3)+q(nq)+EE(16)
+ *            EE as the 4x4 row-major matrix of urdf_fk.py:108       [store_trajectory]
+ *   wnoise   w_eps before / after SavGol (V,H,A)                     */
+mppi_status mppi_get_costs(mppi_engine* e, float* S);
+mppi_status mppi_get_weights(mppi_engine* e, float* w);
+mppi_status mppi_get_noise(mppi_engine* e, float* eps);
+mppi_status mppi_get_trajectory(mppi_engine* e, float* traj);
+mppi_status mppi_get_weighted_noise(mppi_engine* e, float* raw, float* smoothed);
+
+/* Kernel timing with HIP events on the engine stream (bench / roofline). */
+mppi_status mppi_enable_timing(mppi_engine* e, int32_t enable);
+mppi_status mppi_get_timing(mppi_engine* e, double* rollout_ms_total, double* finalize_ms_total,
+                            int64_t* n_rollout, int64_t* n_finalize);
+
+/* Algorithmic HBM bytes one mppi_rollout launch moves. */
+int64_t mppi_rollout_bytes(const mppi_config* cfg);
+
+/* Host-side helpers (no GPU needed): the fp32 constants the engine bakes, exposed so
+ * the CPU test-suite can pin them against the reference fixtures. */
+void mppi_joint_origin(const mppi_joint* j, float* T16);                 /* transformation_matrix.py:28-35 */
+void mppi_base_transform(const double* xyzquat, int32_t f64, float* T16); /* urdf_fk.py:30-55             */
+void mppi_target_rotation(const float* quat_xyzw, float* R9);            /* rotation_conversions.py:45-75 */
+int32_t mppi_savgol_coefficients(int32_t window, int32_t order, float* c); /* svg_filter.py:50-55        */
+/* Host FK of one joint vector (check_reach, urdf_fk.py:60-75); base as xyzquat. */
+mppi_status mppi_host_fk(const mppi_joint* joints, int32_t n_joints, const double* q, const double* xyzquat,
+                         int32_t f64, float* T16);
+
+/* Device RNG check: standard normals z (K,H,A) and raw Philox words (K,H,4*ceil(A/4))
+ * exactly as the rollout kernel draws them for (seed, step, vehicle, global k0..k0+K). */
+mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, int64_t k0, int32_t K,
+                                int32_t H, int32_t A, int32_t device, float* z, uint32_t* raw);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPPI_HIP_H */

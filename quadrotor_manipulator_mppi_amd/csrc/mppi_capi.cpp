@@ -1,0 +1,937 @@
+// mppi_capi.cpp -- host side of libmppi_hip.so: the C-ABI of include/mppi_hip.h.
+//
+// Owns the engine (device buffers allocated once at create, no allocation in
+// the step), bakes the per-joint / per-vehicle fp32 constants exactly the way
+// the reference builds its tensors, and sequences the two kernels of a step on
+// one HIP stream.  See DESIGN.md for the data layout and the kernel roofline.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mppi_dev.h"
+
+using namespace mppi;
+
+namespace {
+
+thread_local std::string g_err;
+
+mppi_status fail(mppi_status st, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail(MPPI_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),      \
+                        __FILE__, __LINE__);                                                       \
+    } while (0)
+
+int pow2ceil(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int nq_of(const mppi_config& c) {
+    if (c.model == MPPI_MODEL_ARM) return c.n_action;
+    if (c.model == MPPI_MODEL_WHOLEBODY) return c.n_action - 3;
+    return 0;
+}
+
+// ----------------------------------------------------- reference fp32 builders
+// rotation_matrix_rpy (transformation_matrix.py:4-25): every product is a 0-d
+// fp32 tensor op, evaluated left to right.
+void rpy_to_R(float r, float p, float y, float* R) {
+    const float cr = cosf(r), sr = sinf(r), cp = cosf(p), sp = sinf(p), cy = cosf(y), sy = sinf(y);
+    volatile float t;   // keep every intermediate an fp32 rounding (no contraction)
+    t = cy * cp; R[0] = t;
+    t = cy * sp; t = t * sr; { volatile float u = sy * cr; R[1] = t - u; }
+    t = cy * sp; t = t * cr; { volatile float u = sy * sr; R[2] = t + u; }
+    t = sy * cp; R[3] = t;
+    t = sy * sp; t = t * sr; { volatile float u = cy * cr; R[4] = t + u; }
+    t = sy * sp; t = t * cr; { volatile float u = cy * sr; R[5] = t - u; }
+    R[6] = -sp;
+    t = cp * sr; R[7] = t;
+    t = cp * cr; R[8] = t;
+}
+
+void joint_origin(const mppi_joint& j, float* T16) {
+    float R[9];
+    rpy_to_R(j.rpy[0], j.rpy[1], j.rpy[2], R);
+    std::memset(T16, 0, 16 * sizeof(float));
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) T16[4 * i + k] = R[3 * i + k];
+    T16[3] = j.xyz[0]; T16[7] = j.xyz[1]; T16[11] = j.xyz[2];
+    T16[15] = 1.0f;
+}
+
+void unit_axis(const mppi_joint& j, float* a) {
+    float x = 1.0f, y = 0.0f, z = 0.0f;
+    if (j.has_axis) { x = j.axis[0]; y = j.axis[1]; z = j.axis[2]; }
+    const float n = sqrtf(x * x + y * y + z * z);
+    if (!(n >= 1e-12f)) { a[0] = 1.0f; a[1] = 0.0f; a[2] = 0.0f; return; }
+    a[0] = x / n; a[1] = y / n; a[2] = z / n;
+}
+
+// xyzquat_to_matrix (urdf_fk.py:30-55) in the state dtype, rounded into fp32.
+template <typename T>
+void base_from_xyzquat_t(const double* b, float* T16) {
+    const T qx = (T)b[3], qy = (T)b[4], qz = (T)b[5], qw = (T)b[6];
+    volatile T a, c;
+    std::memset(T16, 0, 16 * sizeof(float));
+    a = (T)1 - (T)2 * (qy * qy); a = a - (T)2 * (qz * qz); T16[0] = (float)a;
+    a = ((T)2 * qx) * qy; c = ((T)2 * qz) * qw; T16[1] = (float)(a - c);
+    a = ((T)2 * qx) * qz; c = ((T)2 * qy) * qw; T16[2] = (float)(a + c);
+    a = ((T)2 * qx) * qy; c = ((T)2 * qz) * qw; T16[4] = (float)(a + c);
+    a = (T)1 - (T)2 * (qx * qx); a = a - (T)2 * (qz * qz); T16[5] = (float)a;
+    a = ((T)2 * qy) * qz; c = ((T)2 * qx) * qw; T16[6] = (float)(a - c);
+    a = ((T)2 * qx) * qz; c = ((T)2 * qy) * qw; T16[8] = (float)(a - c);
+    a = ((T)2 * qy) * qz; c = ((T)2 * qx) * qw; T16[9] = (float)(a + c);
+    a = (T)1 - (T)2 * (qx * qx); a = a - (T)2 * (qy * qy); T16[10] = (float)a;
+    T16[3] = (float)(T)b[0]; T16[7] = (float)(T)b[1]; T16[11] = (float)(T)b[2];
+    T16[15] = 1.0f;
+}
+
+// quaternion_to_matrix with xyzw input (rotation_conversions.py:45-75), fp32.
+void quat_xyzw_to_R(const float* q, float* R) {
+    const float i = q[0], j = q[1], k = q[2], r = q[3];
+    volatile float s = i * i;
+    s = s + j * j; s = s + k * k; s = s + r * r;
+    const float ts = 2.0f / s;
+    volatile float u;
+    u = j * j + k * k; R[0] = 1.0f - ts * u;
+    u = i * j - k * r; R[1] = ts * u;
+    u = i * k + j * r; R[2] = ts * u;
+    u = i * j + k * r; R[3] = ts * u;
+    u = i * i + k * k; R[4] = 1.0f - ts * u;
+    u = j * k - i * r; R[5] = ts * u;
+    u = i * k - j * r; R[6] = ts * u;
+    u = j * k + i * r; R[7] = ts * u;
+    u = i * i + j * j; R[8] = 1.0f - ts * u;
+}
+
+// ZYX Euler (rotation_conversions.py:277-319): returns (yaw, pitch, roll).
+void euler_zyx(const float* m, float* ypr) {
+    float v = -m[6];
+    v = std::min(1.0f, std::max(-1.0f, v));
+    ypr[1] = asinf(v);
+    ypr[0] = atan2f(m[3], m[0]);
+    ypr[2] = atan2f(m[7], m[8]);
+}
+
+// Savitzky-Golay smoothing taps (svg_filter.py:50-55): first row of
+// inv(A^T A) A^T for the Vandermonde A on x = -h..h (fp64 solve, fp32 taps).
+int savgol_taps(int window, int order, float* c) {
+    if (window < 1 || window % 2 == 0 || window > kMaxW || order < 0 || order >= window) return -1;
+    const int h = window / 2, n = order + 1;
+    double M[16][16] = {}, Minv[16][16] = {};
+    for (int r = 0; r < n; ++r)
+        for (int s = 0; s < n; ++s) {
+            double acc = 0.0;
+            for (int x = -h; x <= h; ++x) acc += std::pow((double)x, r) * std::pow((double)x, s);
+            M[r][s] = acc;
+        }
+    for (int r = 0; r < n; ++r) Minv[r][r] = 1.0;
+    for (int col = 0; col < n; ++col) {   // Gauss-Jordan with partial pivoting
+        int piv = col;
+        for (int r = col + 1; r < n; ++r)
+            if (std::fabs(M[r][col]) > std::fabs(M[piv][col])) piv = r;
+        for (int s = 0; s < n; ++s) { std::swap(M[col][s], M[piv][s]); std::swap(Minv[col][s], Minv[piv][s]); }
+        const double d = M[col][col];
+        for (int s = 0; s < n; ++s) { M[col][s] /= d; Minv[col][s] /= d; }
+        for (int r = 0; r < n; ++r) {
+            if (r == col) continue;
+            const double f = M[r][col];
+            for (int s = 0; s < n; ++s) { M[r][s] -= f * M[col][s]; Minv[r][s] -= f * Minv[col][s]; }
+        }
+    }
+    for (int x = -h; x <= h; ++x) {
+        double acc = 0.0;
+        for (int s = 0; s < n; ++s) acc += Minv[0][s] * std::pow((double)x, s);
+        c[x + h] = (float)acc;
+    }
+    return 0;
+}
+
+void bake_joint(const mppi_joint& j, JointDev& d) {
+    std::memset(&d, 0, sizeof(d));
+    d.type = j.type;
+    d.q_index = j.q_index;
+    float T16[16];
+    joint_origin(j, T16);
+    for (int i = 0; i < 12; ++i) d.O[i] = T16[i];
+    unit_axis(j, d.ax);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) d.axx[3 * r + c] = d.ax[r] * d.ax[c];
+    d.axis_z = (d.ax[0] == 0.0f && d.ax[1] == 0.0f && d.ax[2] == 1.0f) ? 1 : 0;
+}
+
+// Host FK at one joint vector (check_reach path, urdf_fk.py:60-75 +
+// urdfparser.py:166-206): cos/sin in the state dtype, transforms in fp32.
+void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xyzquat, bool f64, float* out16) {
+    float T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    auto mul = [](const float* A, const float* B, float* C) {
+        float r[16];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                float acc = 0.0f;
+                for (int k = 0; k < 4; ++k) acc += A[4 * i + k] * B[4 * k + j];
+                r[4 * i + j] = acc;
+            }
+        std::memcpy(C, r, sizeof(r));
+    };
+    for (int n = 0; n < nj; ++n) {
+        const mppi_joint& j = joints[n];
+        float O[16], L[16];
+        joint_origin(j, O);
+        if (j.type == MPPI_JOINT_REVOLUTE && j.q_index >= 0) {
+            float a[3];
+            unit_axis(j, a);
+            const double qv = f64 ? q[j.q_index] : (double)(float)q[j.q_index];
+            float c, s;
+            if (f64) { c = (float)std::cos(qv); s = (float)std::sin(qv); }
+            else { c = cosf((float)qv); s = sinf((float)qv); }
+            const float omc = 1.0f - c;
+            float R[16] = {c + a[0] * a[0] * omc, a[0] * a[1] * omc - a[2] * s, a[0] * a[2] * omc + a[1] * s, 0,
+                           a[1] * a[0] * omc + a[2] * s, c + a[1] * a[1] * omc, a[1] * a[2] * omc - a[0] * s, 0,
+                           a[2] * a[0] * omc - a[1] * s, a[2] * a[1] * omc + a[0] * s, c + a[2] * a[2] * omc, 0,
+                           0, 0, 0, 1};
+            mul(O, R, L);
+        } else if (j.type == MPPI_JOINT_PRISMATIC && j.q_index >= 0) {
+            float a[3];
+            unit_axis(j, a);
+            const float qf = (float)q[j.q_index];
+            float S[16] = {1, 0, 0, a[0] * qf, 0, 1, 0, a[1] * qf, 0, 0, 1, a[2] * qf, 0, 0, 0, 1};
+            mul(O, S, L);
+        } else {
+            std::memcpy(L, O, sizeof(L));
+        }
+        mul(T, L, T);
+    }
+    float B[16];
+    if (f64) base_from_xyzquat_t<double>(xyzquat, B);
+    else base_from_xyzquat_t<float>(xyzquat, B);
+    mul(B, T, out16);
+}
+
+}  // namespace
+
+// =============================================================================
+struct mppi_engine {
+    mppi_config cfg;
+    int K, H, A, V, nq, qoff, state_dim, out_dim, C, threads;
+    int64_t out_bytes;
+    DevParams dp;
+    FinParams fp;
+    float sg_taps[kMaxW];
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    JointDev* d_joints = nullptr;
+    VehicleConst* d_vc = nullptr;
+    float* d_u_prev = nullptr;
+    float* d_noise_in = nullptr;
+    uint32_t* d_step = nullptr;
+    float* d_traj = nullptr;
+    float* d_noise_out = nullptr;
+    float* d_S = nullptr;
+    float* d_part = nullptr;
+    unsigned char* d_out = nullptr;   // out doubles | u0 floats | stats floats
+    float* d_wraw = nullptr;
+    float* d_wsmooth = nullptr;
+    float* d_w = nullptr;
+    float* d_exchange = nullptr;
+    VehicleConst* h_vc = nullptr;       // pinned staging
+    unsigned char* h_out = nullptr;     // pinned
+    hipEvent_t ev_vc = nullptr, ev_out = nullptr;
+    bool vc_pending = false, state_set = false, out_pending = false;
+    std::vector<float> tpos, tquat;
+    std::vector<double> state;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> roll_pairs, fin_pairs;
+    double roll_ms = 0.0, fin_ms = 0.0;
+    int64_t roll_n = 0, fin_n = 0;
+};
+
+namespace {
+
+mppi_status use_device(mppi_engine* e) {
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    return MPPI_OK;
+}
+
+size_t off_u0(const mppi_engine* e) { return ((size_t)e->V * e->out_dim * sizeof(double) + 15) & ~size_t(15); }
+size_t off_stats(const mppi_engine* e) { return (off_u0(e) + (size_t)e->V * e->A * sizeof(float) + 15) & ~size_t(15); }
+
+mppi_status build_vehicle_consts(mppi_engine* e) {
+    const mppi_config& c = e->cfg;
+    for (int v = 0; v < e->V; ++v) {
+        VehicleConst& vc = e->h_vc[v];
+        std::memset(&vc, 0, sizeof(vc));
+        const double* s = e->state.data() + (size_t)v * e->state_dim;
+        std::memcpy(vc.tpos, &e->tpos[3 * v], 3 * sizeof(float));
+        quat_xyzw_to_R(&e->tquat[4 * v], vc.tR);
+        if (c.model == MPPI_MODEL_DRONE) {
+            for (int a = 0; a < 3; ++a) {
+                vc.pos0f[a] = (float)s[a]; vc.vel0f[a] = (float)s[3 + a];
+                vc.pos0[a] = vc.pos0f[a]; vc.vel0[a] = vc.vel0f[a];
+            }
+        } else if (c.model == MPPI_MODEL_ARM) {
+            float T16[16];
+            if (c.state_f64) base_from_xyzquat_t<double>(s, T16);
+            else base_from_xyzquat_t<float>(s, T16);
+            for (int i = 0; i < 12; ++i) vc.base[i] = T16[i];
+            for (int a = 0; a < e->nq; ++a) {
+                const double q = s[7 + a], qd = s[7 + e->nq + a];
+                vc.pos0f[a] = (float)q; vc.vel0f[a] = (float)qd;
+                vc.pos0[a] = c.state_f64 ? q : (double)vc.pos0f[a];
+                vc.vel0[a] = c.state_f64 ? qd : (double)vc.vel0f[a];
+            }
+        } else {   // whole-body: base pos(3) quat(4) q(nq) base vel(3) qd(nq)
+            float qf[4] = {(float)s[3], (float)s[4], (float)s[5], (float)s[6]};
+            float Rq[9], ypr[3], R[9];
+            quat_xyzw_to_R(qf, Rq);
+            euler_zyx(Rq, ypr);
+            rpy_to_R(ypr[2], ypr[1], ypr[0], R);   // transformation_matrix.py:148-187
+            for (int i = 0; i < 3; ++i)
+                for (int k = 0; k < 3; ++k) vc.base[4 * i + k] = R[3 * i + k];
+            for (int a = 0; a < 3; ++a) {
+                vc.pos0f[a] = (float)s[a]; vc.vel0f[a] = (float)s[7 + e->nq + a];
+            }
+            for (int a = 0; a < e->nq; ++a) {
+                vc.pos0f[3 + a] = (float)s[7 + a]; vc.vel0f[3 + a] = (float)s[7 + e->nq + 3 + a];
+            }
+            for (int a = 0; a < e->A; ++a) { vc.pos0[a] = vc.pos0f[a]; vc.vel0[a] = vc.vel0f[a]; }
+        }
+    }
+    return MPPI_OK;
+}
+
+mppi_status upload_consts(mppi_engine* e) {
+    if (e->vc_pending) {   // the previous copy out of the staging buffer must be done
+        HIP_TRY(hipEventSynchronize(e->ev_vc));
+        e->vc_pending = false;
+    }
+    mppi_status st = build_vehicle_consts(e);
+    if (st != MPPI_OK) return st;
+    HIP_TRY(hipMemcpyAsync(e->d_vc, e->h_vc, sizeof(VehicleConst) * e->V, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipEventRecord(e->ev_vc, e->stream));
+    e->vc_pending = true;
+    return MPPI_OK;
+}
+
+hipEvent_t pool_event(mppi_engine* e) {
+    if (!e->ev_pool.empty()) {
+        hipEvent_t ev = e->ev_pool.back();
+        e->ev_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev = nullptr;
+    (void)hipEventCreate(&ev);
+    return ev;
+}
+
+mppi_status drain_timing(mppi_engine* e) {
+    for (auto* vec : {&e->roll_pairs, &e->fin_pairs}) {
+        for (auto& pr : *vec) {
+            HIP_TRY(hipEventSynchronize(pr.second));
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+            if (vec == &e->roll_pairs) { e->roll_ms += ms; ++e->roll_n; }
+            else { e->fin_ms += ms; ++e->fin_n; }
+            e->ev_pool.push_back(pr.first);
+            e->ev_pool.push_back(pr.second);
+        }
+        vec->clear();
+    }
+    return MPPI_OK;
+}
+
+mppi_status validate(const mppi_config& c) {
+    if (c.model < 0 || c.model > 2) return fail(MPPI_ERR_INVALID_ARG, "unknown model %d", c.model);
+    if (c.n_vehicles < 1 || c.n_samples < 1 || c.n_horizon < 2 || c.n_horizon > MPPI_MAX_HORIZON)
+        return fail(MPPI_ERR_INVALID_ARG, "bad sizes V=%d K=%d H=%d", c.n_vehicles, c.n_samples, c.n_horizon);
+    if (c.model == MPPI_MODEL_DRONE && c.n_action != 3)
+        return fail(MPPI_ERR_INVALID_ARG, "DRONE needs n_action=3");
+    if (c.model == MPPI_MODEL_ARM && c.n_action != 6 && c.n_action != 7)
+        return fail(MPPI_ERR_INVALID_ARG, "ARM supports n_action 6 or 7 (got %d)", c.n_action);
+    if (c.model == MPPI_MODEL_WHOLEBODY && c.n_action != 9 && c.n_action != 10)
+        return fail(MPPI_ERR_INVALID_ARG, "WHOLEBODY supports n_action 9 or 10 (got %d)", c.n_action);
+    if (c.model != MPPI_MODEL_DRONE) {
+        if (c.n_joints < 1 || c.n_joints > MPPI_MAX_JOINTS)
+            return fail(MPPI_ERR_INVALID_ARG, "n_joints=%d", c.n_joints);
+        const int nq = nq_of(c);
+        for (int j = 0; j < c.n_joints; ++j) {
+            const mppi_joint& jj = c.joints[j];
+            if (jj.type < 0 || jj.type > 2) return fail(MPPI_ERR_INVALID_ARG, "joint %d: bad type", j);
+            if (jj.type != MPPI_JOINT_FIXED && (jj.q_index < 0 || jj.q_index >= nq))
+                return fail(MPPI_ERR_INVALID_ARG, "joint %d: q_index %d outside [0,%d)", j, jj.q_index, nq);
+        }
+    }
+    const int half = c.savgol_window / 2;
+    if (c.savgol_window % 2 != 1 || c.savgol_window > kMaxW)
+        return fail(MPPI_ERR_INVALID_ARG, "Window size must be odd (and <= %d).", kMaxW);
+    if (c.savgol_order >= c.savgol_window)
+        return fail(MPPI_ERR_INVALID_ARG, "Polyorder must be less than window size.");
+    if (c.n_horizon <= half)
+        return fail(MPPI_ERR_INVALID_ARG, "Padding (%d) is too large for data length (%d).", half, c.n_horizon);
+    if (!(c.lambda_ > 0.0) || !(c.dt > 0.0)) return fail(MPPI_ERR_INVALID_ARG, "lambda and dt must be > 0");
+    if (c.shard_count < 1 || c.shard_rank < 0 || c.shard_rank >= c.shard_count)
+        return fail(MPPI_ERR_INVALID_ARG, "shard %d/%d", c.shard_rank, c.shard_count);
+    if (c.block_threads && (c.block_threads % 64 || c.block_threads > 512))
+        return fail(MPPI_ERR_INVALID_ARG, "block_threads must be a multiple of 64 <= 512");
+    return MPPI_OK;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+int32_t mppi_abi_version(void) { return MPPI_ABI_VERSION; }
+const char* mppi_last_error(void) { return g_err.c_str(); }
+
+void mppi_struct_sizes(int32_t* c, int32_t* j, int32_t* s) {
+    if (c) *c = (int32_t)sizeof(mppi_config);
+    if (j) *j = (int32_t)sizeof(mppi_joint);
+    if (s) *s = (int32_t)sizeof(mppi_stats);
+}
+
+void mppi_config_default(mppi_config* c, int32_t model) {
+    std::memset(c, 0, sizeof(*c));
+    c->model = model;
+    c->n_vehicles = 1;
+    c->n_horizon = 32;
+    c->dt = 0.01;
+    c->lambda_ = 0.1;
+    c->savgol_order = 2;
+    c->seed = 0x5EEDULL;
+    c->shard_count = 1;
+    c->store_trajectory = 1;
+    c->reach_tol = 0.005f;
+    if (model == MPPI_MODEL_DRONE) {            // drone_mppi.py:16-35, 87-107, 160
+        c->n_samples = 1000; c->n_action = 3;
+        for (int a = 0; a < 3; ++a) c->sigma[a * 3 + a] = 30.0f;
+        c->w_stage_pos = 100.0f; c->w_term_pos = 20.0f;
+        c->savgol_window = 5;
+    } else {                                     // mppi.py:37-75; cost_manager.py:25-28
+        c->n_samples = 100;
+        c->n_action = (model == MPPI_MODEL_ARM) ? 7 : 10;
+        const int A = c->n_action;
+        for (int a = 0; a < A; ++a) c->sigma[a * A + a] = 0.1f;
+        if (model == MPPI_MODEL_WHOLEBODY) {
+            c->n_horizon = 64;
+            for (int a = 0; a < 3; ++a) c->sigma[a * A + a] = 30.0f;
+        }
+        c->w_stage_pos = 50.0f; c->w_stage_ori = 30.0f; c->w_term_pos = 40.0f; c->w_term_ori = 30.0f;
+        c->savgol_window = 9;
+        c->check_reach = (model == MPPI_MODEL_ARM);
+        c->state_f64 = (model == MPPI_MODEL_ARM);
+    }
+}
+
+int32_t mppi_state_dim(const mppi_config* c) {
+    const int nq = nq_of(*c);
+    if (c->model == MPPI_MODEL_DRONE) return 6;
+    if (c->model == MPPI_MODEL_ARM) return 7 + 2 * nq;
+    return 7 + nq + 3 + nq;
+}
+
+int32_t mppi_output_dim(const mppi_config* c) {
+    const int nq = nq_of(*c);
+    if (c->model == MPPI_MODEL_DRONE) return 6;
+    if (c->model == MPPI_MODEL_ARM) return 2 * nq;
+    return 6 + 2 * nq;
+}
+
+int32_t mppi_traj_channels(const mppi_config* c) {
+    if (c->model == MPPI_MODEL_DRONE) return 3;
+    return c->n_action + 16;
+}
+
+int64_t mppi_rollout_bytes(const mppi_config* c) {
+    // algorithmic bytes of one rollout launch: trajectory planes written
+    // (+ injected eps read, + eps written when stored) + S + partial records
+    const int64_t KH = (int64_t)c->n_vehicles * c->n_samples * c->n_horizon;
+    const int64_t C = (c->model == MPPI_MODEL_DRONE) ? 3 : c->n_action + 12;
+    int64_t b = 0;
+    if (c->store_trajectory) b += KH * C * 4;
+    if (c->noise_mode == MPPI_NOISE_INJECTED) b += KH * c->n_action * 4;
+    if (c->store_noise) b += KH * c->n_action * 4;
+    b += (int64_t)c->n_vehicles * c->n_samples * 4;
+    return b;
+}
+
+void mppi_joint_origin(const mppi_joint* j, float* T16) { joint_origin(*j, T16); }
+
+void mppi_base_transform(const double* xyzquat, int32_t f64, float* T16) {
+    if (f64) base_from_xyzquat_t<double>(xyzquat, T16);
+    else base_from_xyzquat_t<float>(xyzquat, T16);
+}
+
+void mppi_target_rotation(const float* q, float* R9) { quat_xyzw_to_R(q, R9); }
+
+int32_t mppi_savgol_coefficients(int32_t window, int32_t order, float* c) { return savgol_taps(window, order, c); }
+
+mppi_status mppi_host_fk(const mppi_joint* joints, int32_t nj, const double* q, const double* xyzquat,
+                         int32_t f64, float* T16) {
+    if (!joints || nj < 0 || nj > MPPI_MAX_JOINTS || !q || !xyzquat || !T16)
+        return fail(MPPI_ERR_INVALID_ARG, "mppi_host_fk: bad arguments");
+    host_fk(joints, nj, q, xyzquat, f64 != 0, T16);
+    return MPPI_OK;
+}
+
+mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
+    if (!cfg || !out) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    mppi_status st = validate(*cfg);
+    if (st != MPPI_OK) return st;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return fail(MPPI_ERR_INVALID_ARG, "device %d not present (%d HIP devices)", cfg->device, ndev);
+
+    mppi_engine* e = new mppi_engine();
+    e->cfg = *cfg;
+    if (e->cfg.model == MPPI_MODEL_WHOLEBODY) e->cfg.state_f64 = 0;
+    const mppi_config& c = e->cfg;
+    e->K = c.n_samples; e->H = c.n_horizon; e->A = c.n_action; e->V = c.n_vehicles;
+    e->nq = nq_of(c);
+    e->qoff = (c.model == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
+    e->state_dim = mppi_state_dim(&c);
+    e->out_dim = mppi_output_dim(&c);
+    e->C = (c.model == MPPI_MODEL_DRONE) ? 3 : e->A + 12;
+    e->tpos.assign((size_t)3 * e->V, 0.0f);
+    e->tquat.assign((size_t)4 * e->V, 0.0f);
+    for (int v = 0; v < e->V; ++v) e->tquat[4 * v + 3] = 1.0f;
+    e->state.assign((size_t)e->state_dim * e->V, 0.0);
+
+    // ---- geometry
+    const int H = e->H;
+    const int L = (H > 64) ? 64 : std::max(16, pow2ceil(H));
+    const int nch = (H + 63) / 64;
+    if (nch != 1 && nch != 2 && nch != 4) {
+        delete e;
+        return fail(MPPI_ERR_INVALID_ARG, "H=%d: supported horizons are <= 128 or 193..256", H);
+    }
+    const int R = 64 / L;
+    e->threads = c.block_threads ? c.block_threads : 256;
+    const int nw = e->threads / 64;
+    const int groups = (e->K + nw * R - 1) / (nw * R);
+    int nb = c.blocks_per_vehicle;
+    if (nb <= 0) nb = std::max(1, std::min(groups, (1024 + e->V - 1) / e->V));
+    nb = std::min(nb, groups);
+    const int iters = (groups + nb - 1) / nb;
+    nb = (groups + iters - 1) / iters;
+    if (nb > 4096) { delete e; return fail(MPPI_ERR_INVALID_ARG, "too many rollout blocks (%d)", nb); }
+    const int P = (kHdr + e->A * H + 3) & ~3;
+
+    if (savgol_taps(c.savgol_window, c.savgol_order, e->sg_taps) != 0) {
+        delete e;
+        return fail(MPPI_ERR_INVALID_ARG, "bad SavGol window/order");
+    }
+
+#define CREATE_TRY(expr)                                                                  \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess) {                                                           \
+            fail(MPPI_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));            \
+            mppi_destroy(e);                                                              \
+            return MPPI_ERR_HIP;                                                          \
+        }                                                                                 \
+    } while (0)
+
+    CREATE_TRY(hipSetDevice(c.device));
+    CREATE_TRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+    e->stream = e->own_stream;
+    CREATE_TRY(hipEventCreateWithFlags(&e->ev_vc, hipEventDisableTiming));
+    CREATE_TRY(hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming));
+    const size_t KH = (size_t)e->V * e->K * H;
+    CREATE_TRY(hipMalloc(&e->d_joints, sizeof(JointDev) * kMaxJ));
+    CREATE_TRY(hipMalloc(&e->d_vc, sizeof(VehicleConst) * e->V));
+    CREATE_TRY(hipMalloc(&e->d_u_prev, sizeof(float) * e->V * H * e->A));
+    CREATE_TRY(hipMalloc(&e->d_step, 64));
+    CREATE_TRY(hipMalloc(&e->d_S, sizeof(float) * e->V * e->K));
+    CREATE_TRY(hipMalloc(&e->d_w, sizeof(float) * e->V * e->K));
+    CREATE_TRY(hipMalloc(&e->d_part, sizeof(float) * (size_t)e->V * nb * P));
+    CREATE_TRY(hipMalloc(&e->d_wraw, sizeof(float) * e->V * H * e->A));
+    CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
+    if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * KH * e->C));
+    if (c.store_noise) CREATE_TRY(hipMalloc(&e->d_noise_out, sizeof(float) * KH * e->A));
+    e->out_bytes = (int64_t)(((size_t)e->V * e->out_dim * 8 + 15) / 16 * 16 + ((size_t)e->V * e->A * 4 + 15) / 16 * 16 +
+                             (size_t)e->V * 16);
+    CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_vc, sizeof(VehicleConst) * e->V, hipHostMallocDefault));
+    CREATE_TRY(hipMemsetAsync(e->d_u_prev, 0, sizeof(float) * e->V * H * e->A, e->stream));
+    CREATE_TRY(hipMemsetAsync(e->d_step, 0, 64, e->stream));
+    CREATE_TRY(hipMemsetAsync(e->d_out, 0, e->out_bytes, e->stream));
+
+    std::vector<JointDev> jd(kMaxJ);
+    for (int j = 0; j < c.n_joints; ++j) bake_joint(c.joints[j], jd[j]);
+    CREATE_TRY(hipMemcpy(e->d_joints, jd.data(), sizeof(JointDev) * kMaxJ, hipMemcpyHostToDevice));
+    CREATE_TRY(hipStreamSynchronize(e->stream));
+#undef CREATE_TRY
+
+    DevParams& p = e->dp;
+    std::memset(&p, 0, sizeof(p));
+    p.model = c.model; p.V = e->V; p.K = e->K; p.H = H; p.A = e->A;
+    p.L = L; p.R = R; p.nch = nch; p.nb = nb; p.iters = iters;
+    p.nq = e->nq; p.qoff = e->qoff; p.nj = c.n_joints;
+    p.noise_mode = c.noise_mode; p.state_f64 = c.state_f64;
+    p.store_traj = c.store_trajectory; p.store_noise = c.store_noise;
+    bool diag = true;
+    for (int a = 0; a < e->A; ++a)
+        for (int b = 0; b < e->A; ++b) {
+            p.sigma[a * e->A + b] = c.sigma[a * e->A + b];
+            if (a != b && c.sigma[a * e->A + b] != 0.0f) diag = false;
+        }
+    p.sigma_diag = diag;
+    p.P = P; p.C = e->C;
+    p.seed_lo = (uint32_t)c.seed; p.seed_hi = (uint32_t)(c.seed >> 32);
+    p.k_offset = (int64_t)c.shard_rank * e->K;
+    p.dt = (float)c.dt; p.dt2 = (float)(c.dt * c.dt); p.dt_d = c.dt;
+    p.coef = (float)(-1.0 / c.lambda_);
+    p.w_sp = c.w_stage_pos; p.w_so = c.w_stage_ori; p.w_tp = c.w_term_pos; p.w_to = c.w_term_ori;
+    p.joints = e->d_joints; p.vc = e->d_vc; p.u_prev = e->d_u_prev; p.step = e->d_step;
+    p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.part = e->d_part;
+
+    FinParams& f = e->fp;
+    std::memset(&f, 0, sizeof(f));
+    f.model = c.model; f.V = e->V; f.H = H; f.A = e->A; f.nq = e->nq; f.qoff = e->qoff;
+    f.state_f64 = c.state_f64; f.P = P;
+    f.window = c.savgol_window; f.half = c.savgol_window / 2;
+    for (int j = 0; j < c.savgol_window; ++j) f.sg[j] = e->sg_taps[c.savgol_window - 1 - j];
+    f.coef = p.coef; f.dt = p.dt; f.dt2 = p.dt2; f.dt_d = c.dt;
+    f.u_prev = e->d_u_prev; f.vc = e->d_vc;
+    f.out = (double*)e->d_out;
+    f.u0 = (float*)(e->d_out + off_u0(e));
+    f.stats = (float*)(e->d_out + off_stats(e));
+    f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.step = e->d_step; f.out_dim = e->out_dim;
+    *out = e;
+    return MPPI_OK;
+}
+
+void mppi_destroy(mppi_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->cfg.device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& pr : e->roll_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    void* dev[] = {e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_step, e->d_traj, e->d_noise_out,
+                   e->d_S, e->d_part, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w};
+    for (void* p : dev) if (p) (void)hipFree(p);
+    if (e->h_out) (void)hipHostFree(e->h_out);
+    if (e->h_vc) (void)hipHostFree(e->h_vc);
+    if (e->ev_vc) (void)hipEventDestroy(e->ev_vc);
+    if (e->ev_out) (void)hipEventDestroy(e->ev_out);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    delete e;
+}
+
+mppi_status mppi_set_stream(mppi_engine* e, void* s) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->stream = s ? (hipStream_t)s : e->own_stream;
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_target(mppi_engine* e, int32_t v, const float* pos, const float* quat) {
+    if (!e || !pos || v < 0 || v >= e->V) return fail(MPPI_ERR_INVALID_ARG, "mppi_set_target: bad arguments");
+    std::memcpy(&e->tpos[3 * v], pos, 3 * sizeof(float));
+    if (quat) std::memcpy(&e->tquat[4 * v], quat, 4 * sizeof(float));
+    if (e->state_set) {
+        if (use_device(e)) return MPPI_ERR_HIP;
+        return upload_consts(e);
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_u_prev(mppi_engine* e, const float* u) {
+    if (!e || !u) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipMemcpyAsync(e->d_u_prev, u, sizeof(float) * e->V * e->H * e->A, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_u_prev(mppi_engine* e, float* u) {
+    if (!e || !u) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipMemcpyAsync(u, e->d_u_prev, sizeof(float) * e->V * e->H * e->A, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_state(mppi_engine* e, const double* state) {
+    if (!e || !state) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    std::memcpy(e->state.data(), state, sizeof(double) * e->state.size());
+    e->state_set = true;
+    return upload_consts(e);
+}
+
+mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(e->d_step, &step, sizeof(step), hipMemcpyHostToDevice));
+    return MPPI_OK;
+}
+
+mppi_status mppi_exchange_slot_floats(mppi_engine* e, int64_t* n) {
+    if (!e || !n) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    *n = (int64_t)e->V * e->dp.P;
+    return MPPI_OK;
+}
+
+mppi_status mppi_bind_exchange(mppi_engine* e, float* d) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    e->d_exchange = d;
+    return MPPI_OK;
+}
+
+mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_rollout before mppi_set_state");
+    if (e->cfg.noise_mode == MPPI_NOISE_INJECTED && !d_noise)
+        return fail(MPPI_ERR_INVALID_ARG, "INJECTED noise mode needs a device noise buffer");
+    if (e->cfg.shard_count > 1 && !e->d_exchange)
+        return fail(MPPI_ERR_STATE, "shard_count > 1 needs mppi_bind_exchange");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    DevParams p = e->dp;
+    p.noise_in = d_noise;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
+    int rc = mppi_launch_rollout(&p, e->threads, e->stream);
+    if (rc != 0) return fail(MPPI_ERR_HIP, "rollout launch failed (%d: %s)", rc,
+                             rc > 0 ? hipGetErrorString((hipError_t)rc) : "no kernel for this model/A/H");
+    if (e->timing) {
+        HIP_TRY(hipEventRecord(e1, e->stream));
+        e->roll_pairs.emplace_back(e0, e1);
+        if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
+    }
+    if (e->cfg.shard_count > 1) {   // fold this shard's block records into its exchange slot
+        const size_t slot = (size_t)e->V * e->dp.P;
+        HIP_TRY(hipMemsetAsync(e->d_exchange, 0, sizeof(float) * slot * e->cfg.shard_count, e->stream));
+        FinParams f = e->fp;
+        f.mode = 1;
+        f.rec = e->d_part; f.nrec = e->dp.nb;
+        f.rec_vstride = (int64_t)e->dp.nb * e->dp.P; f.rec_rstride = e->dp.P;
+        f.dst = e->d_exchange + slot * e->cfg.shard_rank;
+        rc = mppi_launch_finalize(&f, e->stream);
+        if (rc != 0) return fail(MPPI_ERR_HIP, "pack launch failed (%d)", rc);
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_finalize(mppi_engine* e) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    FinParams f = e->fp;
+    f.mode = 0;
+    if (e->cfg.shard_count > 1) {
+        f.rec = e->d_exchange; f.nrec = e->cfg.shard_count;
+        f.rec_vstride = e->dp.P; f.rec_rstride = (int64_t)e->V * e->dp.P;
+    } else {
+        f.rec = e->d_part; f.nrec = e->dp.nb;
+        f.rec_vstride = (int64_t)e->dp.nb * e->dp.P; f.rec_rstride = e->dp.P;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
+    int rc = mppi_launch_finalize(&f, e->stream);
+    if (rc != 0) return fail(MPPI_ERR_HIP, "finalize launch failed (%d)", rc);
+    if (e->timing) { HIP_TRY(hipEventRecord(e1, e->stream)); e->fin_pairs.emplace_back(e0, e1); }
+    HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipEventRecord(e->ev_out, e->stream));
+    e->out_pending = true;
+    return MPPI_OK;
+}
+
+mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->out_pending) return fail(MPPI_ERR_STATE, "no finalised step to read");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipEventSynchronize(e->ev_out));
+    const double* o = (const double*)e->h_out;
+    const float* uu = (const float*)(e->h_out + off_u0(e));
+    const float* st = (const float*)(e->h_out + off_stats(e));
+    if (out) std::memcpy(out, o, sizeof(double) * e->V * e->out_dim);
+    if (u0) std::memcpy(u0, uu, sizeof(float) * e->V * e->A);
+    bool nonfinite = false;
+    for (int v = 0; v < e->V; ++v) {
+        int reach = 0;
+        if (e->cfg.check_reach && e->cfg.model == MPPI_MODEL_ARM) {   // mppi.py:95-120 (host FK)
+            const double* s = e->state.data() + (size_t)v * e->state_dim;
+            const double* qdes = o + (size_t)v * e->out_dim;
+            float T16[16];
+            host_fk(e->cfg.joints, e->cfg.n_joints, qdes, s, e->cfg.state_f64 != 0, T16);
+            const float err = std::fabs(T16[3] - e->tpos[3 * v]) + std::fabs(T16[7] - e->tpos[3 * v + 1]) +
+                              std::fabs(T16[11] - e->tpos[3 * v + 2]);
+            reach = err < e->cfg.reach_tol;
+        }
+        const int nf = (st[4 * v + 3] > 0.0f) || !std::isfinite(st[4 * v]) || !std::isfinite(uu[(size_t)v * e->A]);
+        nonfinite |= nf;
+        if (stats) {
+            stats[v].rho = st[4 * v];
+            stats[v].eta = st[4 * v + 1];
+            stats[v].ess = st[4 * v + 2];
+            stats[v].nonfinite = nf;
+            stats[v].reach = reach;
+            stats[v]._pad = 0;
+        }
+    }
+    (void)nonfinite;   // the reference propagates NaN silently; callers read stats.nonfinite
+    return MPPI_OK;
+}
+
+mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out, float* u0,
+                      mppi_stats* stats) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_step is single-shard; use the split phases");
+    mppi_status st;
+    if (state && (st = mppi_set_state(e, state)) != MPPI_OK) return st;
+    const float* dn = nullptr;
+    if (e->cfg.noise_mode == MPPI_NOISE_INJECTED) {
+        if (!h_noise) return fail(MPPI_ERR_INVALID_ARG, "INJECTED noise mode needs noise");
+        const size_t n = (size_t)e->V * e->K * e->H * e->A;
+        if (use_device(e)) return MPPI_ERR_HIP;
+        if (!e->d_noise_in) HIP_TRY(hipMalloc(&e->d_noise_in, n * sizeof(float)));
+        HIP_TRY(hipMemcpyAsync(e->d_noise_in, h_noise, n * sizeof(float), hipMemcpyHostToDevice, e->stream));
+        dn = e->d_noise_in;
+    }
+    if ((st = mppi_rollout(e, dn)) != MPPI_OK) return st;
+    if ((st = mppi_finalize(e)) != MPPI_OK) return st;
+    return mppi_read_outputs(e, out, u0, stats);
+}
+
+mppi_status mppi_synchronize(mppi_engine* e) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_costs(mppi_engine* e, float* S) {
+    if (!e || !S) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipMemcpyAsync(S, e->d_S, sizeof(float) * e->V * e->K, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_weights(mppi_engine* e, float* w) {
+    if (!e || !w) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    int rc = mppi_launch_weights(e->d_S, e->fp.stats, e->d_w, e->V, e->K, e->dp.coef, e->stream);
+    if (rc) return fail(MPPI_ERR_HIP, "weights launch failed (%d)", rc);
+    HIP_TRY(hipMemcpyAsync(w, e->d_w, sizeof(float) * e->V * e->K, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_noise(mppi_engine* e, float* eps) {
+    if (!e || !eps) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->d_noise_out) return fail(MPPI_ERR_STATE, "engine created without store_noise");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipMemcpyAsync(eps, e->d_noise_out, sizeof(float) * (size_t)e->V * e->K * e->H * e->A,
+                           hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_trajectory(mppi_engine* e, float* traj) {
+    if (!e || !traj) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->d_traj) return fail(MPPI_ERR_STATE, "engine created without store_trajectory");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t KH = (size_t)e->K * e->H, n = (size_t)e->V * e->C * KH;
+    std::vector<float> soa(n);
+    HIP_TRY(hipMemcpyAsync(soa.data(), e->d_traj, n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const int Cr = mppi_traj_channels(&e->cfg);
+    const int nstate = (e->cfg.model == MPPI_MODEL_DRONE) ? 3 : e->A;
+    for (int v = 0; v < e->V; ++v)
+        for (size_t i = 0; i < KH; ++i) {
+            float* dst = traj + ((size_t)v * KH + i) * Cr;
+            const float* src = soa.data() + (size_t)v * e->C * KH + i;
+            for (int c = 0; c < nstate; ++c) dst[c] = src[c * KH];
+            if (e->cfg.model != MPPI_MODEL_DRONE) {
+                float* ee = dst + nstate;
+                for (int r = 0; r < 12; ++r) ee[r] = src[(nstate + r) * KH];
+                ee[12] = 0.0f; ee[13] = 0.0f; ee[14] = 0.0f; ee[15] = 1.0f;
+            }
+        }
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_weighted_noise(mppi_engine* e, float* raw, float* smoothed) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t n = sizeof(float) * e->V * e->H * e->A;
+    if (raw) HIP_TRY(hipMemcpyAsync(raw, e->d_wraw, n, hipMemcpyDeviceToHost, e->stream));
+    if (smoothed) HIP_TRY(hipMemcpyAsync(smoothed, e->d_wsmooth, n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_enable_timing(mppi_engine* e, int32_t enable) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    mppi_status st = drain_timing(e);
+    if (st) return st;
+    e->timing = enable != 0;
+    e->roll_ms = e->fin_ms = 0.0;
+    e->roll_n = e->fin_n = 0;
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_timing(mppi_engine* e, double* rms, double* fms, int64_t* rn, int64_t* fn) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    mppi_status st = drain_timing(e);
+    if (st) return st;
+    if (rms) *rms = e->roll_ms;
+    if (fms) *fms = e->fin_ms;
+    if (rn) *rn = e->roll_n;
+    if (fn) *fn = e->fin_n;
+    return MPPI_OK;
+}
+
+mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, int64_t k0, int32_t K, int32_t H,
+                                int32_t A, int32_t device, float* z, uint32_t* raw) {
+    if (K < 1 || H < 1 || A < 1 || A > MPPI_MAX_ACTION || !z || !raw)
+        return fail(MPPI_ERR_INVALID_ARG, "mppi_philox_normals: bad arguments");
+    HIP_TRY(hipSetDevice(device));
+    const size_t n = (size_t)K * H;
+    const int nj = (A + 3) / 4;
+    float* dz = nullptr;
+    uint32_t* dr = nullptr;
+    HIP_TRY(hipMalloc(&dz, n * A * sizeof(float)));
+    HIP_TRY(hipMalloc(&dr, n * nj * 4 * sizeof(uint32_t)));
+    int rc = mppi_launch_philox(seed, step, vehicle, k0, K, H, A, dz, dr, nullptr);
+    hipError_t e1 = hipMemcpy(z, dz, n * A * sizeof(float), hipMemcpyDeviceToHost);
+    hipError_t e2 = hipMemcpy(raw, dr, n * nj * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(dz);
+    (void)hipFree(dr);
+    if (rc) return fail(MPPI_ERR_HIP, "philox launch failed (%d)", rc);
+    if (e1 != hipSuccess || e2 != hipSuccess) return fail(MPPI_ERR_HIP, "philox copy failed");
+    return MPPI_OK;
+}
+
+}  // extern "C"

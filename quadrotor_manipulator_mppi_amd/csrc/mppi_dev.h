@@ -1,0 +1,108 @@
+// mppi_dev.h -- structures shared by the host C-ABI (mppi_capi.cpp) and the
+// gfx950 kernels (mppi_kernels.hip).  Internal: not part of the public ABI.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/mppi_hip.h"
+
+namespace mppi {
+
+constexpr int kMaxA = MPPI_MAX_ACTION;
+constexpr int kMaxJ = MPPI_MAX_JOINTS;
+constexpr int kMaxW = MPPI_MAX_SAVGOL;
+constexpr int kHdr = 4;  // partial record header: rho, eta, eta2, pad
+
+// One joint of the chain, pre-baked on the host exactly the way the reference
+// builds its tensors (transformation_matrix.py:28-35, 58-95).
+struct JointDev {
+    int32_t type;      // mppi_joint_type
+    int32_t q_index;   // -1 = not actuated
+    int32_t axis_z;    // 1 if the unit axis is exactly (0,0,1): fast Rodrigues
+    int32_t _pad;
+    float O[12];       // origin transform rows 0..2 (3x4, row-major), fp32 as torch builds it
+    float ax[3];       // unit axis (fp32, axis / ||axis||)
+    float axx[9];      // fl(a_i * a_j) products as the reference evaluates vx*vx etc.
+};
+
+// Per-vehicle constants derived on the host from state + target (uploaded with
+// every mppi_set_state; everything the rollout needs that is uniform per vehicle).
+struct VehicleConst {
+    double pos0[kMaxA];   // initial positions per action dim (drone xyz / joints / both)
+    double vel0[kMaxA];   // initial velocities
+    float pos0f[kMaxA];   // fp32 copies (f32 state mode)
+    float vel0f[kMaxA];
+    float base[12];       // ARM: fp32 base transform rows 0..2 (urdf_fk.py:30-55)
+                          // WB : rotation (cols 0..2) from rpy(quat) (transformation_matrix.py:148-187)
+    float tpos[3];        // target position
+    float tR[9];          // target rotation (quaternion_to_matrix, xyzw)
+    float _pad[3];
+};
+
+struct DevParams {
+    int32_t model, V, K, H, A;
+    int32_t L;          // lanes per rollout segment (pow2 >= H, <= 64)
+    int32_t R;          // rollouts per wave = 64 / L
+    int32_t nch;        // 64-lane chunks per rollout when H > 64 (else 1)
+    int32_t nb;         // rollout blocks per vehicle
+    int32_t iters;      // rollout groups per block
+    int32_t nq;         // arm joints (0 for drone)
+    int32_t qoff;       // first arm dim in the action vector (0 arm, 3 whole-body)
+    int32_t nj;         // joints in the chain
+    int32_t noise_mode, state_f64, store_traj, store_noise;
+    int32_t sigma_diag;
+    int32_t P;          // floats per partial record (kHdr + A*H, rounded up to 4)
+    int32_t C;          // stored trajectory channels (EE as 12)
+    uint32_t seed_lo, seed_hi;
+    int64_t k_offset;   // global index of this shard's first sample
+    float dt, dt2;      // fp32(dt), fp32(dt**2)
+    double dt_d;        // dt as double (fp64-promoted path)
+    float coef;         // fp32(-1/lambda)
+    float w_sp, w_so, w_tp, w_to;
+    float sigma[kMaxA * kMaxA];
+    // device pointers
+    const JointDev* joints;
+    const VehicleConst* vc;
+    const float* u_prev;     // (V,H,A)
+    const float* noise_in;   // (V,K,H,A) injected
+    const uint32_t* step;    // device step counter
+    float* traj;             // (V,C,K,H) SoA planes
+    float* noise_out;        // (V,K,H,A)
+    float* S;                // (V,K)
+    float* part;             // (V,nb,P)
+};
+
+// Finalize / pack kernel parameters.
+struct FinParams {
+    int32_t model, V, H, A, nq, qoff, state_f64;
+    int32_t nrec;            // records to combine per vehicle
+    int64_t rec_vstride, rec_rstride;   // floats
+    int32_t P;
+    int32_t mode;            // 0 = final, 1 = pack into dst slot
+    int32_t window, half;
+    float coef, dt, dt2;
+    double dt_d;
+    float sg[kMaxW];         // SavGol taps (already flipped for the correlation)
+    const float* rec;        // records base
+    float* dst;              // pack destination (slot base, vehicle stride P)
+    float* u_prev;           // (V,H,A) in/out
+    const VehicleConst* vc;
+    double* out;             // (V, out_dim)
+    float* u0;               // (V, A)
+    float* stats;            // (V, 4): rho, eta, ess, nonfinite
+    float* wraw;             // (V,H,A) readback
+    float* wsmooth;          // (V,H,A) readback
+    uint32_t* step;          // incremented once per final step
+    int32_t out_dim;
+};
+
+}  // namespace mppi
+
+// launchers (mppi_kernels.hip)
+extern "C" {
+int mppi_launch_rollout(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_finalize(const mppi::FinParams* p, void* stream);
+int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int K, float coef,
+                        void* stream);
+int mppi_launch_philox(uint64_t seed, uint32_t step, int vehicle, int64_t k0, int K, int H, int A,
+                       float* z, uint32_t* raw, void* stream);
+}

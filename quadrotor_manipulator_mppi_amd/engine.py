@@ -1,0 +1,252 @@
+"""Python handle on one libmppi_hip.so engine.
+
+Thin host-side plumbing over the C-ABI (``include/mppi_hip.h``): it fills the
+config struct, keeps numpy staging arrays, and turns status codes into
+exceptions.  All arithmetic of the control step runs in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _capi as capi
+from .robot.urdf_chain import load_chain
+
+MODELS = {"drone": capi.MODEL_DRONE, "arm": capi.MODEL_ARM, "wholebody": capi.MODEL_WHOLEBODY}
+JOINT_TYPES = {"fixed": capi.JOINT_FIXED, "revolute": capi.JOINT_REVOLUTE,
+               "continuous": capi.JOINT_REVOLUTE, "prismatic": capi.JOINT_PRISMATIC}
+
+
+@dataclass
+class StepStats:
+    rho: float
+    eta: float
+    ess: float
+    nonfinite: bool
+    reach: bool
+
+
+def fill_joints(cfg: capi.Config, chain: Sequence[Dict]) -> None:
+    if len(chain) > capi.MAX_JOINTS:
+        raise ValueError(f"chain has {len(chain)} joints (max {capi.MAX_JOINTS})")
+    cfg.n_joints = len(chain)
+    for i, j in enumerate(chain):
+        J = cfg.joints[i]
+        J.type = JOINT_TYPES.get(j["type"], capi.JOINT_FIXED)
+        J.q_index = int(j.get("q_index", -1))
+        for d in range(3):
+            J.xyz[d] = float(j["xyz"][d])
+            J.rpy[d] = float(j["rpy"][d])
+        ax = j.get("axis")
+        J.has_axis = 0 if ax is None else 1
+        if ax is not None:
+            for d in range(3):
+                J.axis[d] = float(ax[d])
+
+
+def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: Optional[int] = None,
+                n_vehicles: int = 1, n_action: Optional[int] = None, dt: float = 0.01, lam: float = 0.1,
+                sigma=None, weights: Optional[Sequence[float]] = None, chain=None,
+                savgol_window: Optional[int] = None, savgol_order: int = 2, noise: str = "philox",
+                seed: int = 0x5EED, device: int = 0, shard_rank: int = 0, shard_count: int = 1,
+                state_f64: Optional[bool] = None, store_trajectory: bool = True, store_noise: bool = False,
+                check_reach: Optional[bool] = None, reach_tol: float = 0.005, blocks_per_vehicle: int = 0,
+                block_threads: int = 0) -> capi.Config:
+    L = capi.lib()
+    cfg = capi.Config()
+    L.mppi_config_default(C.byref(cfg), MODELS[model])
+    cfg.n_vehicles = n_vehicles
+    if n_samples is not None:
+        cfg.n_samples = n_samples
+    if n_horizon is not None:
+        cfg.n_horizon = n_horizon
+    if n_action is not None:
+        cfg.n_action = n_action
+    cfg.dt, cfg.lambda_ = dt, lam
+    A = cfg.n_action
+    if sigma is not None:
+        s = np.asarray(sigma, np.float32)
+        if s.ndim == 1:
+            s = np.diag(s)
+        if s.shape != (A, A):
+            raise ValueError(f"sigma must be ({A},{A})")
+        for i in range(A * A):
+            cfg.sigma[i] = float(s.reshape(-1)[i])
+    if weights is not None:
+        cfg.w_stage_pos, cfg.w_stage_ori, cfg.w_term_pos, cfg.w_term_ori = map(float, weights)
+    if model != "drone":
+        fill_joints(cfg, chain if chain is not None else load_chain())
+    if savgol_window is not None:
+        cfg.savgol_window = savgol_window
+    cfg.savgol_order = savgol_order
+    cfg.noise_mode = capi.NOISE_INJECTED if noise == "injected" else capi.NOISE_PHILOX
+    cfg.seed = seed
+    cfg.device = device
+    cfg.shard_rank, cfg.shard_count = shard_rank, shard_count
+    if state_f64 is not None:
+        cfg.state_f64 = int(state_f64)
+    cfg.store_trajectory = int(store_trajectory)
+    cfg.store_noise = int(store_noise)
+    if check_reach is not None:
+        cfg.check_reach = int(check_reach)
+    cfg.reach_tol = reach_tol
+    cfg.blocks_per_vehicle = blocks_per_vehicle
+    cfg.block_threads = block_threads
+    return cfg
+
+
+class Engine:
+    """One MPPI engine on one GPU (V vehicles x K samples x H steps)."""
+
+    def __init__(self, cfg: Optional[capi.Config] = None, **kw):
+        self._L = capi.lib()
+        self.cfg = cfg if cfg is not None else make_config(**kw)
+        h = C.c_void_p()
+        capi.check(self._L.mppi_create(C.byref(self.cfg), C.byref(h)), "mppi_create")
+        self._h = h
+        c = self.cfg
+        self.V, self.K, self.H, self.A = c.n_vehicles, c.n_samples, c.n_horizon, c.n_action
+        self.state_dim = self._L.mppi_state_dim(C.byref(c))
+        self.out_dim = self._L.mppi_output_dim(C.byref(c))
+        self.traj_channels = self._L.mppi_traj_channels(C.byref(c))
+        self._out = np.zeros((self.V, self.out_dim), np.float64)
+        self._u0 = np.zeros((self.V, self.A), np.float32)
+        self._stats = (capi.Stats * self.V)()
+
+    # ------------------------------------------------------------------ admin
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mppi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int):
+        capi.check(self._L.mppi_set_stream(self._h, C.c_void_p(stream_handle)), "set_stream")
+
+    def set_target(self, pos, quat=None, vehicle: int = 0):
+        p = np.ascontiguousarray(pos, np.float32).reshape(3)
+        q = None if quat is None else np.ascontiguousarray(quat, np.float32).reshape(4)
+        capi.check(self._L.mppi_set_target(self._h, vehicle, capi.fptr(p), capi.fptr(q)), "set_target")
+
+    def set_u_prev(self, u):
+        u = np.ascontiguousarray(u, np.float32).reshape(self.V, self.H, self.A)
+        capi.check(self._L.mppi_set_u_prev(self._h, capi.fptr(u)), "set_u_prev")
+
+    def get_u_prev(self) -> np.ndarray:
+        u = np.empty((self.V, self.H, self.A), np.float32)
+        capi.check(self._L.mppi_get_u_prev(self._h, capi.fptr(u)), "get_u_prev")
+        return u
+
+    def set_state(self, state):
+        s = np.ascontiguousarray(state, np.float64).reshape(self.V, self.state_dim)
+        capi.check(self._L.mppi_set_state(self._h, capi.dptr(s)), "set_state")
+
+    def set_step_counter(self, step: int):
+        capi.check(self._L.mppi_set_step_counter(self._h, step & 0xFFFFFFFF), "set_step_counter")
+
+    # ------------------------------------------------------------------- step
+    def step(self, state=None, noise=None):
+        """One control step: returns (out (V,out_dim) float64, u0 (V,A), [StepStats])."""
+        s = None if state is None else np.ascontiguousarray(state, np.float64).reshape(self.V, self.state_dim)
+        n = None if noise is None else np.ascontiguousarray(noise, np.float32).reshape(
+            self.V, self.K, self.H, self.A)
+        capi.check(self._L.mppi_step(self._h, capi.dptr(s), capi.fptr(n), capi.dptr(self._out),
+                                     capi.fptr(self._u0), self._stats), "mppi_step")
+        return self._out.copy(), self._u0.copy(), self.stats()
+
+    def rollout(self, d_noise_ptr: int = 0):
+        capi.check(self._L.mppi_rollout(self._h, C.c_void_p(d_noise_ptr or None)), "rollout")
+
+    def finalize(self):
+        capi.check(self._L.mppi_finalize(self._h), "finalize")
+
+    def read_outputs(self):
+        capi.check(self._L.mppi_read_outputs(self._h, capi.dptr(self._out), capi.fptr(self._u0),
+                                             self._stats), "read_outputs")
+        return self._out.copy(), self._u0.copy(), self.stats()
+
+    def synchronize(self):
+        capi.check(self._L.mppi_synchronize(self._h), "synchronize")
+
+    def stats(self) -> List[StepStats]:
+        return [StepStats(s.rho, s.eta, s.ess, bool(s.nonfinite), bool(s.reach)) for s in self._stats]
+
+    # -------------------------------------------------------------- exchange
+    def exchange_slot_floats(self) -> int:
+        n = C.c_int64()
+        capi.check(self._L.mppi_exchange_slot_floats(self._h, C.byref(n)), "exchange_slot_floats")
+        return n.value
+
+    def bind_exchange(self, d_ptr: int):
+        capi.check(self._L.mppi_bind_exchange(self._h, C.c_void_p(d_ptr)), "bind_exchange")
+
+    # -------------------------------------------------------------- readback
+    def get_costs(self) -> np.ndarray:
+        S = np.empty((self.V, self.K), np.float32)
+        capi.check(self._L.mppi_get_costs(self._h, capi.fptr(S)), "get_costs")
+        return S
+
+    def get_weights(self) -> np.ndarray:
+        w = np.empty((self.V, self.K), np.float32)
+        capi.check(self._L.mppi_get_weights(self._h, capi.fptr(w)), "get_weights")
+        return w
+
+    def get_noise(self) -> np.ndarray:
+        e = np.empty((self.V, self.K, self.H, self.A), np.float32)
+        capi.check(self._L.mppi_get_noise(self._h, capi.fptr(e)), "get_noise")
+        return e
+
+    def get_trajectory(self) -> np.ndarray:
+        t = np.empty((self.V, self.K, self.H, self.traj_channels), np.float32)
+        capi.check(self._L.mppi_get_trajectory(self._h, capi.fptr(t)), "get_trajectory")
+        return t
+
+    def get_weighted_noise(self):
+        raw = np.empty((self.V, self.H, self.A), np.float32)
+        sm = np.empty_like(raw)
+        capi.check(self._L.mppi_get_weighted_noise(self._h, capi.fptr(raw), capi.fptr(sm)), "get_weighted_noise")
+        return raw, sm
+
+    # ---------------------------------------------------------------- timing
+    def enable_timing(self, on: bool = True):
+        capi.check(self._L.mppi_enable_timing(self._h, int(on)), "enable_timing")
+
+    def timing(self):
+        r, f = C.c_double(), C.c_double()
+        rn, fn = C.c_int64(), C.c_int64()
+        capi.check(self._L.mppi_get_timing(self._h, C.byref(r), C.byref(f), C.byref(rn), C.byref(fn)), "timing")
+        return {"rollout_ms_total": r.value, "finalize_ms_total": f.value,
+                "n_rollout": rn.value, "n_finalize": fn.value}
+
+    def rollout_bytes(self) -> int:
+        return int(self._L.mppi_rollout_bytes(C.byref(self.cfg)))
+
+
+def philox_normals(seed: int, step: int, vehicle: int, k0: int, K: int, H: int, A: int, device: int = 0):
+    L = capi.lib()
+    z = np.empty((K, H, A), np.float32)
+    raw = np.empty((K, H, 4 * ((A + 3) // 4)), np.uint32)
+    capi.check(L.mppi_philox_normals(seed, step, vehicle, k0, K, H, A, device, capi.fptr(z),
+                                     raw.ctypes.data_as(C.POINTER(C.c_uint32))), "philox_normals")
+    return raw, z
+
+
+def host_fk(chain, q, xyzquat, f64: bool = True) -> np.ndarray:
+    """Single-configuration FK on the host (the check_reach path)."""
+    L = capi.lib()
+    cfg = capi.Config()
+    fill_joints(cfg, chain)
+    qq = np.ascontiguousarray(q, np.float64)
+    b = np.ascontiguousarray(xyzquat, np.float64)
+    T = np.empty(16, np.float32)
+    capi.check(L.mppi_host_fk(cfg.joints, cfg.n_joints, capi.dptr(qq), capi.dptr(b), int(f64),
+                              capi.fptr(T)), "host_fk")
+    return T.reshape(4, 4)

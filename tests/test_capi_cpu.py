@@ -1,0 +1,146 @@
+"""CPU-side checks of the C-ABI library: it loads, exports exactly what
+``include/mppi_hip.h`` declares, its struct layout matches the binding, and the
+host-side fp32 constants it bakes match the reference fixtures.  No GPU calls."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+from oracle import mppi_oracle as O
+from quadrotor_manipulator_mppi_amd import _capi as capi
+from quadrotor_manipulator_mppi_amd.engine import fill_joints, host_fk, make_config
+from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain, parse_urdf_chain
+
+HEADER = os.path.join(ROOT, "include", "mppi_hip.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mppi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = capi.lib()
+    names = _declared()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(L, n), f"libmppi_hip.so does not export {n}"
+    assert set(names) == set(capi.PROTOTYPES), "binding and header disagree"
+
+
+def test_struct_layout_matches_header():
+    L = capi.lib()
+    s = [C.c_int32(), C.c_int32(), C.c_int32()]
+    L.mppi_struct_sizes(*[C.byref(x) for x in s])
+    assert (s[0].value, s[1].value, s[2].value) == (C.sizeof(capi.Config), C.sizeof(capi.Joint),
+                                                  C.sizeof(capi.Stats))
+
+
+def test_config_defaults_are_reference_values():
+    L = capi.lib()
+    c = capi.Config()
+    L.mppi_config_default(C.byref(c), capi.MODEL_DRONE)      # drone_mppi.py:16-35
+    assert (c.n_samples, c.n_horizon, c.n_action, c.dt, c.lambda_) == (1000, 32, 3, 0.01, 0.1)
+    assert c.sigma[0] == 30.0 and c.sigma[4] == 30.0 and c.sigma[1] == 0.0
+    assert (c.w_stage_pos, c.w_term_pos, c.savgol_window) == (100.0, 20.0, 5)
+    L.mppi_config_default(C.byref(c), capi.MODEL_ARM)        # mppi.py:37-75, cost_manager.py:25-28
+    assert (c.n_samples, c.n_horizon, c.n_action) == (100, 32, 7)
+    assert abs(c.sigma[0] - 0.1) < 1e-8 and c.sigma[8] == c.sigma[0]
+    assert (c.w_stage_pos, c.w_stage_ori, c.w_term_pos, c.w_term_ori) == (50.0, 30.0, 40.0, 30.0)
+    assert c.savgol_window == 9 and c.check_reach == 1 and abs(c.reach_tol - 0.005) < 1e-9
+    assert L.mppi_state_dim(C.byref(c)) == 21 and L.mppi_output_dim(C.byref(c)) == 14
+
+
+def test_shipped_chain_matches_urdf_parse(tmp_path):
+    """The shipped joint table equals a fresh parse of the chain the reference
+    walks (root 'base' -> 'j2s7s300_link_7', mppi.py:84-88)."""
+    chain = load_chain()
+    assert [j["type"] for j in chain] == ["fixed"] + ["revolute"] * 7
+    assert [j["q_index"] for j in chain] == [-1, 0, 1, 2, 3, 4, 5, 6]
+    urdf = "/root/reference/src/aerial_manipulation/urdf/aerial_manipulator_gpu.urdf"
+    if os.path.exists(urdf):
+        assert parse_urdf_chain(urdf, "base", "j2s7s300_link_7") == chain
+
+
+def test_joint_origins_match_reference(kinova_chain):
+    L = capi.lib()
+    g = load_golden("fk_known_answer.npz")
+    cfg = capi.Config()
+    fill_joints(cfg, load_chain())
+    for i in range(cfg.n_joints):
+        T = np.empty(16, np.float32)
+        L.mppi_joint_origin(C.byref(cfg.joints[i]), capi.fptr(T))
+        np.testing.assert_array_equal(T.reshape(4, 4), g["origins"][i])
+
+
+@pytest.mark.parametrize("f64", [False, True])
+def test_base_transform_matches_oracle(f64):
+    L = capi.lib()
+    g = load_golden("fk_known_answer.npz")
+    for b in g["bases"].astype(np.float64):
+        T = np.empty(16, np.float32)
+        L.mppi_base_transform(capi.dptr(np.ascontiguousarray(b)), int(f64), capi.fptr(T))
+        ref = O.xyzquat_matrix(torch.tensor(b, dtype=torch.float64 if f64 else torch.float32)).numpy()
+        np.testing.assert_array_equal(T.reshape(4, 4), ref)
+
+
+def test_target_rotation_matches_reference():
+    L = capi.lib()
+    g = load_golden("rotations.npz")
+    R = np.empty(9, np.float32)
+    q = np.array([-0.5, -0.5, 0.5, -0.5], np.float32)
+    L.mppi_target_rotation(capi.fptr(q), capi.fptr(R))
+    np.testing.assert_array_equal(R.reshape(3, 3), g["target_R"])
+    for quat, ref in zip(g["quat"][:64], g["quat_R"][:64]):
+        L.mppi_target_rotation(capi.fptr(np.ascontiguousarray(quat)), capi.fptr(R))
+        np.testing.assert_allclose(R.reshape(3, 3), ref, rtol=0, atol=3e-7)
+
+
+def test_savgol_coefficients_match_reference():
+    L = capi.lib()
+    g = load_golden("savgol.npz")
+    for key in [k for k in g if k.startswith("coef_")]:
+        W, P = map(int, key.split("_")[1:])
+        c = np.empty(W, np.float32)
+        assert L.mppi_savgol_coefficients(W, P, capi.fptr(c)) == 0
+        np.testing.assert_allclose(c, g[key], rtol=0, atol=2e-7)
+    assert L.mppi_savgol_coefficients(4, 2, capi.fptr(np.empty(8, np.float32))) != 0   # even window
+
+
+@pytest.mark.parametrize("b", range(4))
+def test_host_fk_matches_reference_cpu_fk(b):
+    g = load_golden("fk_known_answer.npz")
+    chain = load_chain()
+    for j in range(4):
+        q = g["q32"][0, j].astype(np.float64)
+        T = host_fk(chain, q, g["bases"][b].astype(np.float64), f64=False)
+        np.testing.assert_allclose(T, g[f"eecpu_b{b}"][j], rtol=0, atol=2e-6)
+
+
+def test_config_validation_messages():
+    cfg = make_config("arm", n_samples=16, n_horizon=3)      # SavGol pad 4 > H=3
+    h = C.c_void_p()
+    st = capi.lib().mppi_create(C.byref(cfg), C.byref(h))
+    assert st == capi.ERR_INVALID_ARG
+    assert "Padding (4) is too large for data length (3)" in capi.lib().mppi_last_error().decode()
+    cfg = make_config("drone", n_samples=16, savgol_window=4)
+    assert capi.lib().mppi_create(C.byref(cfg), C.byref(h)) == capi.ERR_INVALID_ARG
+    assert "Window size must be odd" in capi.lib().mppi_last_error().decode()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_engine_fails_loudly_without_gpu():
+    from quadrotor_manipulator_mppi_amd.engine import Engine
+    with pytest.raises(capi.MPPIError):
+        Engine(make_config("drone", n_samples=64))
+
+
+def test_rollout_bytes_formula():
+    cfg = make_config("arm", n_samples=4096, n_horizon=32)
+    # trajectory planes (7 q + 12 EE floats) + S per rollout
+    assert capi.lib().mppi_rollout_bytes(C.byref(cfg)) == 4096 * 32 * 19 * 4 + 4096 * 4
