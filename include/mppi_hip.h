@@ -179,6 +179,11 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out,
                       float* u0, mppi_stats* stats);
 
+/* n back-to-back asynchronous control steps (rollout + finalize each, device
+ * noise, state and warm start resident on the GPU); single-shard engines only.
+ * No host synchronisation: pair with mppi_synchronize / mppi_read_outputs. */
+mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
+
 mppi_status mppi_synchronize(mppi_engine* e);
 
 /* Readback in the reference's layouts (synchronous):

@@ -18,6 +18,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libmppi_hip.so")
+LIB_STAMPS = os.path.join(LIB_DIR, "libmppi_hip_stamps.so")   # diagnostic phase-stamp build
 SOURCES = ["mppi_kernels.hip", "mppi_capi.cpp"]
 HEADERS = ["mppi_dev.h", os.path.join("..", "..", "include", "mppi_hip.h")]
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
@@ -38,15 +39,16 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, debug: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, debug: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    out = LIB_STAMPS if stamps else LIB
+    if not force and not stamps and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
            "-O1" if debug else "-O3", "-I", os.path.join(ROOT, "include"),
            "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-o", tmp] + (["-DMPPI_STAMPS"] if stamps else []) + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -54,14 +56,15 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> st
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     if verbose and res.stderr.strip():
         print(res.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic build with per-phase s_memtime stamps")
     a = ap.parse_args()
-    print(build(force=a.force or True, debug=a.debug, verbose=True))
+    print(build(force=a.force or True, debug=a.debug, verbose=True, stamps=a.stamps))
     sys.exit(0)

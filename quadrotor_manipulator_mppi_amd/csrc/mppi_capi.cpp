@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -180,6 +181,19 @@ void bake_joint(const mppi_joint& j, JointDev& d) {
     d.axis_z = (d.ax[0] == 0.0f && d.ax[1] == 0.0f && d.ax[2] == 1.0f) ? 1 : 0;
 }
 
+// C = A * B for 3x4 affine rows (implicit last row 0 0 0 1), fp32.
+void mul34(const float* A, const float* B, float* C) {
+    float r[12];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 4; ++j) {
+            float acc = A[4 * i] * B[j] + A[4 * i + 1] * B[4 + j] + A[4 * i + 2] * B[8 + j];
+            if (j == 3) acc += A[4 * i + 3];
+            r[4 * i + j] = acc;
+        }
+    }
+    std::memcpy(C, r, sizeof(r));
+}
+
 // Host FK at one joint vector (check_reach path, urdf_fk.py:60-75 +
 // urdfparser.py:166-206): cos/sin in the state dtype, transforms in fp32.
 void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xyzquat, bool f64, float* out16) {
@@ -238,12 +252,14 @@ struct mppi_engine {
     DevParams dp;
     FinParams fp;
     float sg_taps[kMaxW];
+    float fixedM[12];                   // product of the leading fixed joints (folded into base)
     hipStream_t own_stream = nullptr, stream = nullptr;
+    float* d_sigma = nullptr;
     JointDev* d_joints = nullptr;
     VehicleConst* d_vc = nullptr;
     float* d_u_prev = nullptr;
     float* d_noise_in = nullptr;
-    uint32_t* d_step = nullptr;
+    uint32_t step_ctr = 0;              // Philox counter word; +1 per finalized step
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
     float* d_S = nullptr;
@@ -254,7 +270,8 @@ struct mppi_engine {
     float* d_w = nullptr;
     float* d_exchange = nullptr;
     VehicleConst* h_vc = nullptr;       // pinned staging
-    unsigned char* h_out = nullptr;     // pinned
+    unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
+    unsigned char* h_out_dev = nullptr; // device view of h_out
     hipEvent_t ev_vc = nullptr, ev_out = nullptr;
     bool vc_pending = false, state_set = false, out_pending = false;
     std::vector<float> tpos, tquat;
@@ -264,6 +281,13 @@ struct mppi_engine {
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> roll_pairs, fin_pairs;
     double roll_ms = 0.0, fin_ms = 0.0;
+    unsigned long long* d_stamps = nullptr;    // MPPI_STAMPS diagnostics
+    unsigned long long* d_fstamps = nullptr;
+    std::vector<double> fstamp_sum;
+    int64_t fstamp_n = 0;
+    std::vector<double> stamp_sum;
+    int64_t stamp_n = 0;
+    double clk_sum = 0.0;
     int64_t roll_n = 0, fin_n = 0;
 };
 
@@ -294,7 +318,7 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
             float T16[16];
             if (c.state_f64) base_from_xyzquat_t<double>(s, T16);
             else base_from_xyzquat_t<float>(s, T16);
-            for (int i = 0; i < 12; ++i) vc.base[i] = T16[i];
+            mul34(T16, e->fixedM, vc.base);
             for (int a = 0; a < e->nq; ++a) {
                 const double q = s[7 + a], qd = s[7 + e->nq + a];
                 vc.pos0f[a] = (float)q; vc.vel0f[a] = (float)qd;
@@ -307,8 +331,8 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
             quat_xyzw_to_R(qf, Rq);
             euler_zyx(Rq, ypr);
             rpy_to_R(ypr[2], ypr[1], ypr[0], R);   // transformation_matrix.py:148-187
-            for (int i = 0; i < 3; ++i)
-                for (int k = 0; k < 3; ++k) vc.base[4 * i + k] = R[3 * i + k];
+            float B[12] = {R[0], R[1], R[2], 0.0f, R[3], R[4], R[5], 0.0f, R[6], R[7], R[8], 0.0f};
+            mul34(B, e->fixedM, vc.base);    // translation column: R * M_t; p(k,t) added on device
             for (int a = 0; a < 3; ++a) {
                 vc.pos0f[a] = (float)s[a]; vc.vel0f[a] = (float)s[7 + e->nq + a];
             }
@@ -328,6 +352,7 @@ mppi_status upload_consts(mppi_engine* e) {
     }
     mppi_status st = build_vehicle_consts(e);
     if (st != MPPI_OK) return st;
+    if (e->V == 1) return MPPI_OK;   // passed by value in the kernel arguments
     HIP_TRY(hipMemcpyAsync(e->d_vc, e->h_vc, sizeof(VehicleConst) * e->V, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(e->ev_vc, e->stream));
     e->vc_pending = true;
@@ -522,14 +547,14 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
 
     // ---- geometry
     const int H = e->H;
-    const int L = (H > 64) ? 64 : std::max(16, pow2ceil(H));
+    const int L = (H > 32) ? 64 : 32;
     const int nch = (H + 63) / 64;
     if (nch != 1 && nch != 2 && nch != 4) {
         delete e;
         return fail(MPPI_ERR_INVALID_ARG, "H=%d: supported horizons are <= 128 or 193..256", H);
     }
     const int R = 64 / L;
-    e->threads = c.block_threads ? c.block_threads : 256;
+    e->threads = c.block_threads ? c.block_threads : 512;
     const int nw = e->threads / 64;
     const int groups = (e->K + nw * R - 1) / (nw * R);
     int nb = c.blocks_per_vehicle;
@@ -564,7 +589,6 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_joints, sizeof(JointDev) * kMaxJ));
     CREATE_TRY(hipMalloc(&e->d_vc, sizeof(VehicleConst) * e->V));
     CREATE_TRY(hipMalloc(&e->d_u_prev, sizeof(float) * e->V * H * e->A));
-    CREATE_TRY(hipMalloc(&e->d_step, 64));
     CREATE_TRY(hipMalloc(&e->d_S, sizeof(float) * e->V * e->K));
     CREATE_TRY(hipMalloc(&e->d_w, sizeof(float) * e->V * e->K));
     CREATE_TRY(hipMalloc(&e->d_part, sizeof(float) * (size_t)e->V * nb * P));
@@ -575,14 +599,25 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     e->out_bytes = (int64_t)(((size_t)e->V * e->out_dim * 8 + 15) / 16 * 16 + ((size_t)e->V * e->A * 4 + 15) / 16 * 16 +
                              (size_t)e->V * 16);
     CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
-    CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    CREATE_TRY(hipHostGetDevicePointer((void**)&e->h_out_dev, e->h_out, 0));
+    std::memset(e->h_out, 0, e->out_bytes);
+    CREATE_TRY(hipMalloc(&e->d_sigma, sizeof(float) * kMaxA * kMaxA));
+    CREATE_TRY(hipMemcpy(e->d_sigma, c.sigma, sizeof(float) * e->A * e->A, hipMemcpyHostToDevice));
     CREATE_TRY(hipHostMalloc((void**)&e->h_vc, sizeof(VehicleConst) * e->V, hipHostMallocDefault));
     CREATE_TRY(hipMemsetAsync(e->d_u_prev, 0, sizeof(float) * e->V * H * e->A, e->stream));
-    CREATE_TRY(hipMemsetAsync(e->d_step, 0, 64, e->stream));
     CREATE_TRY(hipMemsetAsync(e->d_out, 0, e->out_bytes, e->stream));
 
     std::vector<JointDev> jd(kMaxJ);
     for (int j = 0; j < c.n_joints; ++j) bake_joint(c.joints[j], jd[j]);
+    // fold the leading fixed joints of the chain into the per-vehicle base transform
+    const float I12[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    std::memcpy(e->fixedM, I12, sizeof(I12));
+    int j0 = 0;
+    while (c.model != MPPI_MODEL_DRONE && j0 < c.n_joints && jd[j0].type == MPPI_JOINT_FIXED) {
+        mul34(e->fixedM, jd[j0].O, e->fixedM);
+        ++j0;
+    }
     CREATE_TRY(hipMemcpy(e->d_joints, jd.data(), sizeof(JointDev) * kMaxJ, hipMemcpyHostToDevice));
     CREATE_TRY(hipStreamSynchronize(e->stream));
 #undef CREATE_TRY
@@ -597,18 +632,36 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     bool diag = true;
     for (int a = 0; a < e->A; ++a)
         for (int b = 0; b < e->A; ++b) {
-            p.sigma[a * e->A + b] = c.sigma[a * e->A + b];
-            if (a != b && c.sigma[a * e->A + b] != 0.0f) diag = false;
+            if (a == b) p.sdiag[a] = c.sigma[a * e->A + b];
+            else if (c.sigma[a * e->A + b] != 0.0f) diag = false;
         }
     p.sigma_diag = diag;
+    p.sigma = e->d_sigma;
+    p.j0 = j0;
+    {   // fast FK path: the unfolded chain is exactly nq revolute-z joints in q order
+        bool fast = c.model != MPPI_MODEL_DRONE && (c.n_joints - j0) == e->nq;
+        for (int j = j0; fast && j < c.n_joints; ++j)
+            fast = jd[j].type == MPPI_JOINT_REVOLUTE && jd[j].axis_z && jd[j].q_index == j - j0;
+        p.chain_fast = fast;
+    }
     p.P = P; p.C = e->C;
     p.seed_lo = (uint32_t)c.seed; p.seed_hi = (uint32_t)(c.seed >> 32);
     p.k_offset = (int64_t)c.shard_rank * e->K;
     p.dt = (float)c.dt; p.dt2 = (float)(c.dt * c.dt); p.dt_d = c.dt;
     p.coef = (float)(-1.0 / c.lambda_);
     p.w_sp = c.w_stage_pos; p.w_so = c.w_stage_ori; p.w_tp = c.w_term_pos; p.w_to = c.w_term_ori;
-    p.joints = e->d_joints; p.vc = e->d_vc; p.u_prev = e->d_u_prev; p.step = e->d_step;
+    for (int j = 0; j < kMaxJ; ++j) p.joints[j] = jd[j];
+    p.vc = e->d_vc; p.u_prev = e->d_u_prev;
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.part = e->d_part;
+#ifdef MPPI_STAMPS
+    if (getenv("MPPI_STAMPS")) {
+        const size_t nwaves = (size_t)e->V * nb * (e->threads / 64);
+        if (hipMalloc(&e->d_stamps, nwaves * kStamps * 8) == hipSuccess) p.stamps = e->d_stamps;
+        e->stamp_sum.assign(kStamps, 0.0);
+        (void)hipMalloc(&e->d_fstamps, (size_t)e->V * e->A * kStamps * 8);
+        e->fstamp_sum.assign(kStamps, 0.0);
+    }
+#endif
 
     FinParams& f = e->fp;
     std::memset(&f, 0, sizeof(f));
@@ -618,22 +671,37 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     for (int j = 0; j < c.savgol_window; ++j) f.sg[j] = e->sg_taps[c.savgol_window - 1 - j];
     f.coef = p.coef; f.dt = p.dt; f.dt2 = p.dt2; f.dt_d = c.dt;
     f.u_prev = e->d_u_prev; f.vc = e->d_vc;
-    f.out = (double*)e->d_out;
-    f.u0 = (float*)(e->d_out + off_u0(e));
-    f.stats = (float*)(e->d_out + off_stats(e));
-    f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.step = e->d_step; f.out_dim = e->out_dim;
+    f.out = (double*)e->h_out_dev;
+    f.u0 = (float*)(e->h_out_dev + off_u0(e));
+    f.stats = (float*)(e->h_out_dev + off_stats(e));
+    f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.out_dim = e->out_dim;
+    if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
+    f.stamps = e->d_fstamps;
     *out = e;
     return MPPI_OK;
 }
 
 void mppi_destroy(mppi_engine* e) {
     if (!e) return;
+    if (e->d_stamps && e->stamp_n) {
+        static const char* names[] = {"", "lds-init", "noise", "integrator", "fk+cost", "S+softmin(rest)",
+                                      "combine-barrier", "record"};
+        fprintf(stderr, "[mppi stamps] avg cycles per wave over %lld waves:", (long long)e->stamp_n);
+        for (int i = 1; i <= 7; ++i) fprintf(stderr, " %s=%.0f", names[i], e->stamp_sum[i] / e->stamp_n);
+        fprintf(stderr, "\n");
+        static const char* fn[] = {"", "loads", "accum", "eta-reduce", "col-reduce", "final-col", "outputs"};
+        fprintf(stderr, "[mppi stamps] finalize avg cycles per block over %lld blocks:", (long long)e->fstamp_n);
+        for (int i = 1; i <= 6; ++i) fprintf(stderr, " %s=%.0f", fn[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
+        fprintf(stderr, "\n");
+        (void)hipFree(e->d_stamps);
+        (void)hipFree(e->d_fstamps);
+    }
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto& pr : e->roll_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
-    void* dev[] = {e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_step, e->d_traj, e->d_noise_out,
+    void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_part, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
@@ -690,8 +758,7 @@ mppi_status mppi_set_state(mppi_engine* e, const double* state) {
 mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    HIP_TRY(hipMemcpy(e->d_step, &step, sizeof(step), hipMemcpyHostToDevice));
+    e->step_ctr = step;
     return MPPI_OK;
 }
 
@@ -717,6 +784,8 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     if (use_device(e)) return MPPI_ERR_HIP;
     DevParams p = e->dp;
     p.noise_in = d_noise;
+    p.vc0 = e->h_vc[0];
+    p.step_ctr = e->step_ctr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
     int rc = mppi_launch_rollout(&p, e->threads, e->stream);
@@ -731,6 +800,7 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         const size_t slot = (size_t)e->V * e->dp.P;
         HIP_TRY(hipMemsetAsync(e->d_exchange, 0, sizeof(float) * slot * e->cfg.shard_count, e->stream));
         FinParams f = e->fp;
+        f.vc0 = e->h_vc[0];
         f.mode = 1;
         f.rec = e->d_part; f.nrec = e->dp.nb;
         f.rec_vstride = (int64_t)e->dp.nb * e->dp.P; f.rec_rstride = e->dp.P;
@@ -745,6 +815,7 @@ mppi_status mppi_finalize(mppi_engine* e) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
     FinParams f = e->fp;
+    f.vc0 = e->h_vc[0];
     f.mode = 0;
     if (e->cfg.shard_count > 1) {
         f.rec = e->d_exchange; f.nrec = e->cfg.shard_count;
@@ -758,8 +829,8 @@ mppi_status mppi_finalize(mppi_engine* e) {
     int rc = mppi_launch_finalize(&f, e->stream);
     if (rc != 0) return fail(MPPI_ERR_HIP, "finalize launch failed (%d)", rc);
     if (e->timing) { HIP_TRY(hipEventRecord(e1, e->stream)); e->fin_pairs.emplace_back(e0, e1); }
-    HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, e->out_bytes, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipEventRecord(e->ev_out, e->stream));
+    HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
+    ++e->step_ctr;
     e->out_pending = true;
     return MPPI_OK;
 }
@@ -769,6 +840,24 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
     if (!e->out_pending) return fail(MPPI_ERR_STATE, "no finalised step to read");
     if (use_device(e)) return MPPI_ERR_HIP;
     HIP_TRY(hipEventSynchronize(e->ev_out));
+    if (e->d_stamps) {   // diagnostic: average phase cycles over all waves
+        const size_t nwaves = (size_t)e->V * e->dp.nb * (e->threads / 64);
+        std::vector<unsigned long long> st(nwaves * kStamps);
+        HIP_TRY(hipMemcpy(st.data(), e->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+        for (size_t w = 0; w < nwaves; ++w) {
+            const unsigned long long* x = &st[w * kStamps];
+            for (int i = 1; i <= 7; ++i) e->stamp_sum[i] += (double)(x[i] - x[i - 1]);
+        }
+        // clock: wave 0 shader cycles vs 100 MHz realtime across the wave lifetime is not
+        // stamped at the end; report cycles only
+        e->stamp_n += (int64_t)nwaves;
+        const size_t nfb = (size_t)e->V * e->A;
+        std::vector<unsigned long long> fs(nfb * kStamps);
+        HIP_TRY(hipMemcpy(fs.data(), e->d_fstamps, fs.size() * 8, hipMemcpyDeviceToHost));
+        for (size_t b = 0; b < nfb; ++b)
+            for (int i = 1; i <= 6; ++i) e->fstamp_sum[i] += (double)(fs[b * kStamps + i] - fs[b * kStamps + i - 1]);
+        e->fstamp_n += (int64_t)nfb;
+    }
     const double* o = (const double*)e->h_out;
     const float* uu = (const float*)(e->h_out + off_u0(e));
     const float* st = (const float*)(e->h_out + off_stats(e));
@@ -819,6 +908,18 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
     if ((st = mppi_rollout(e, dn)) != MPPI_OK) return st;
     if ((st = mppi_finalize(e)) != MPPI_OK) return st;
     return mppi_read_outputs(e, out, u0, stats);
+}
+
+mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
+    if (!e || n < 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_run_steps: bad arguments");
+    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_run_steps is single-shard");
+    if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_run_steps needs device noise");
+    for (int i = 0; i < n; ++i) {
+        mppi_status st = mppi_rollout(e, nullptr);
+        if (st != MPPI_OK) return st;
+        if ((st = mppi_finalize(e)) != MPPI_OK) return st;
+    }
+    return MPPI_OK;
 }
 
 mppi_status mppi_synchronize(mppi_engine* e) {

@@ -31,12 +31,15 @@ struct VehicleConst {
     double vel0[kMaxA];   // initial velocities
     float pos0f[kMaxA];   // fp32 copies (f32 state mode)
     float vel0f[kMaxA];
-    float base[12];       // ARM: fp32 base transform rows 0..2 (urdf_fk.py:30-55)
-                          // WB : rotation (cols 0..2) from rpy(quat) (transformation_matrix.py:148-187)
+    float base[12];       // ARM: fp32 base transform (urdf_fk.py:30-55) times the leading fixed
+                          //      joints of the chain, rows 0..2
+                          // WB : R(rpy(quat)) (transformation_matrix.py:148-187) times the leading
+                          //      fixed joints; column 3 = R * (their translation), p(k,t) is added
     float tpos[3];        // target position
     float tR[9];          // target rotation (quaternion_to_matrix, xyzw)
-    float _pad[3];
+    float _pad[4];        // sizeof = 496 (16-byte multiple: keeps the dynamic LDS base aligned)
 };
+static_assert(sizeof(VehicleConst) % 16 == 0, "VehicleConst must be a 16-byte multiple");
 
 struct DevParams {
     int32_t model, V, K, H, A;
@@ -50,6 +53,8 @@ struct DevParams {
     int32_t nj;         // joints in the chain
     int32_t noise_mode, state_f64, store_traj, store_noise;
     int32_t sigma_diag;
+    int32_t j0;         // first chain joint not folded into VehicleConst::base
+    int32_t chain_fast; // joints j0.. are nq revolute-z joints with q_index 0..nq-1 in order
     int32_t P;          // floats per partial record (kHdr + A*H, rounded up to 4)
     int32_t C;          // stored trajectory channels (EE as 12)
     uint32_t seed_lo, seed_hi;
@@ -58,18 +63,22 @@ struct DevParams {
     double dt_d;        // dt as double (fp64-promoted path)
     float coef;         // fp32(-1/lambda)
     float w_sp, w_so, w_tp, w_to;
-    float sigma[kMaxA * kMaxA];
+    float sdiag[kMaxA];      // diagonal of Sigma (sigma_diag)
+    VehicleConst vc0;        // vehicle 0 constants by value (V == 1: no upload per step)
+    JointDev joints[kMaxJ];  // chain table by value: uniform scalar (s_load) reads in the FK loop
     // device pointers
-    const JointDev* joints;
-    const VehicleConst* vc;
+    const float* sigma;      // (A,A) full Sigma
+    const VehicleConst* vc;  // (V) when V > 1
     const float* u_prev;     // (V,H,A)
     const float* noise_in;   // (V,K,H,A) injected
-    const uint32_t* step;    // device step counter
+    uint32_t step_ctr;       // control-step index: the Philox counter word (host-counted)
     float* traj;             // (V,C,K,H) SoA planes
     float* noise_out;        // (V,K,H,A)
     float* S;                // (V,K)
     float* part;             // (V,nb,P)
+    unsigned long long* stamps;   // diagnostic s_memtime stamps per wave (MPPI_STAMPS), else null
 };
+constexpr int kStamps = 10;
 
 // Finalize / pack kernel parameters.
 struct FinParams {
@@ -82,17 +91,19 @@ struct FinParams {
     float coef, dt, dt2;
     double dt_d;
     float sg[kMaxW];         // SavGol taps (already flipped for the correlation)
+    VehicleConst vc0;        // V == 1
     const float* rec;        // records base
     float* dst;              // pack destination (slot base, vehicle stride P)
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;
-    double* out;             // (V, out_dim)
-    float* u0;               // (V, A)
-    float* stats;            // (V, 4): rho, eta, ess, nonfinite
+    double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)
+    float* u0;               // (V, A)         -- "
+    float* stats;            // (V, 4): rho, eta, ess, nonfinite -- "
     float* wraw;             // (V,H,A) readback
     float* wsmooth;          // (V,H,A) readback
-    uint32_t* step;          // incremented once per final step
     int32_t out_dim;
+    int32_t dbg;             // diagnostic phase-skip bits (MPPI_FIN_DEBUG), 0 in production
+    unsigned long long* stamps;   // diagnostic s_memtime stamps (MPPI_STAMPS), else null
 };
 
 }  // namespace mppi

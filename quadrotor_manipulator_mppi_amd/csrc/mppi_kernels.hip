@@ -27,6 +27,16 @@ using namespace mppi;
 
 namespace {
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
+// (lgkmcnt) but NOT for its outstanding global stores (vmcnt), which
+// __syncthreads() would drain -- nothing in these kernels reads its own
+// trajectory / record stores back, so the store round trip stays off the
+// critical path.  The memory clobber keeps the compiler from moving LDS
+// accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ----------------------------------------------------------------- DPP helpers
 // dpp_ctrl encodings (GFX9): row_shr:n = 0x110+n, wave_shr:1 = 0x138,
 // row_bcast:15 = 0x142, row_bcast:31 = 0x143.
@@ -65,10 +75,10 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;   // one v_mad_u64_u32 each
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     }
 }
 
@@ -153,18 +163,51 @@ __device__ __forceinline__ void mul_prismatic(Mat34& T, const JointDev& J, float
         T.m[4 * i + 3] += T.m[4 * i] * d0 + T.m[4 * i + 1] * d1 + T.m[4 * i + 2] * d2;
 }
 
-// sin/cos of the joint angle.  fp32 state: the fp32 angle.  fp64 state: the
-// reference evaluates cos/sin in fp64 and rounds into the fp32 transform
-// (transformation_matrix.py:68-93 with q promoted by mppi.py:197), so split the
-// double angle into hi+lo floats and correct to first order.
-__device__ __forceinline__ void joint_sincos(double qd, float qf, bool f64, float& s, float& c) {
-    if (!f64) { sincosf(qf, &s, &c); return; }
-    const float qh = (float)qd;
-    const float ql = (float)(qd - (double)qh);
-    float sh, ch;
-    sincosf(qh, &sh, &ch);
-    s = fmaf(ch, ql, sh);
-    c = fmaf(-sh, ql, ch);
+// sin/cos of a joint angle.  The reference evaluates them in the state dtype
+// (fp32, or fp64 when update_joint got float64 arrays, mppi.py:197) and rounds
+// into the fp32 transform (transformation_matrix.py:68-93).  Cody-Waite
+// reduction by pi/2 in fp64 (exact for |q| << 2^20), then minimax polynomials
+// in fp32 on [-pi/4, pi/4] (Cephes sinf/cosf): ~25 VALU ops, <= 2 ulp, no
+// large-argument path (ocml sincosf is ~130 ops with a Payne-Hanek branch).
+__device__ __forceinline__ void sincos_joint(double q, float& s, float& c) {
+    const double n = rint(q * 0.63661977236758134308);
+    double r = fma(-n, 1.5707963267948966192, q);
+    r = fma(-n, 6.123233995736766036e-17, r);
+    const float x = (float)r, x2 = x * x;
+    float sp = fmaf(x2, -1.9515295891e-4f, 8.3321608736e-3f);
+    sp = fmaf(x2, sp, -1.6666654611e-1f);
+    const float sn = fmaf(x * x2, sp, x);
+    float cp = fmaf(x2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    cp = fmaf(x2, cp, 4.166664568298827e-2f);
+    const float cs = fmaf(x2 * x2, cp, fmaf(-0.5f, x2, 1.0f));
+    const int qd = (int)n & 3;
+    s = (qd & 1) ? cs : sn;
+    c = (qd & 1) ? sn : cs;
+    if (qd & 2) s = -s;
+    if ((qd + 1) & 2) c = -c;
+}
+
+// atan2 with octant reduction and a degree-8 odd minimax polynomial on [0,1]
+// (SLEEF atanf coefficients): ~25 ops, <= 3.5 ulp (ocml atan2f: 45 ops).
+__device__ __forceinline__ float atan2_fast(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float rc = __builtin_amdgcn_rcpf(mx);
+    rc = rc * fmaf(-mx, rc, 2.0f);
+    const float a = (mx > 0.0f) ? mn * rc : 0.0f;
+    const float t = a * a;
+    float u = 0.00282363896258175373077393f;
+    u = fmaf(u, t, -0.0159569028764963150024414f);
+    u = fmaf(u, t, 0.0425049886107444763183594f);
+    u = fmaf(u, t, -0.0748900920152664184570312f);
+    u = fmaf(u, t, 0.106347933411598205566406f);
+    u = fmaf(u, t, -0.142027363181114196777344f);
+    u = fmaf(u, t, 0.199926957488059997558594f);
+    u = fmaf(u, t, -0.333331018686294555664062f);
+    float r = fmaf(a * t, u, a);
+    if (ay > ax) r = 1.57079632679489661923f - r;
+    if (__builtin_signbit(x)) r = 3.14159265358979323846f - r;
+    return __builtin_copysignf(r, y);
 }
 
 // Pose cost of one (k,t): w_pos*||p - p*|| + w_ori*||eulerZYX(R^T R*)||
@@ -172,17 +215,17 @@ __device__ __forceinline__ void joint_sincos(double qd, float qf, bool f64, floa
 // orthonormal FK rotation taken as R^T).
 __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& vc, float wp, float wo) {
     const float dx = T.m[3] - vc.tpos[0], dy = T.m[7] - vc.tpos[1], dz = T.m[11] - vc.tpos[2];
-    const float cp = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+    const float cp = __builtin_amdgcn_sqrtf(dx * dx + dy * dy + dz * dz);
     const float* tR = vc.tR;
     const float r00 = T.m[0] * tR[0] + T.m[4] * tR[3] + T.m[8] * tR[6];
     const float r10 = T.m[1] * tR[0] + T.m[5] * tR[3] + T.m[9] * tR[6];
     const float r20 = T.m[2] * tR[0] + T.m[6] * tR[3] + T.m[10] * tR[6];
     const float r21 = T.m[2] * tR[1] + T.m[6] * tR[4] + T.m[10] * tR[7];
     const float r22 = T.m[2] * tR[2] + T.m[6] * tR[5] + T.m[10] * tR[8];
-    const float yaw = atan2f(r10, r00);
+    const float yaw = atan2_fast(r10, r00);
     const float pitch = asinf(fminf(fmaxf(-r20, -1.0f), 1.0f));
-    const float roll = atan2f(r21, r22);
-    const float co = __builtin_sqrtf(yaw * yaw + pitch * pitch + roll * roll);
+    const float roll = atan2_fast(r21, r22);
+    const float co = __builtin_amdgcn_sqrtf(yaw * yaw + pitch * pitch + roll * roll);
     return wp * cp + wo * co;
 }
 
@@ -191,387 +234,651 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 // =============================================================================
 // k_rollout
 // =============================================================================
-template <int MODEL, int NA, int NCH>
-__global__ void __launch_bounds__(512) k_rollout(const DevParams p) {
+// Diagnostic phase stamps (build with -DMPPI_STAMPS; see tools/stamps.md):
+// s_memtime per wave between scheduling barriers.  Compiled out otherwise.
+#ifdef MPPI_STAMPS
+#define STAMP(i)                                                                                      \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        if (pk.stamps && lane == 0) {                                                                 \
+            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memtime();                             \
+        }                                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+
+// DPP helpers with bound_ctrl (out-of-row sources read 0): no zeroing moves.
+template <int CTRL>
+__device__ __forceinline__ double shr_f64(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(x), __double2loint(x), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(x), __double2hiint(x), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+// Inclusive prefix sum in fp64 inside L-lane segments (Kogge-Stone over DPP):
+// torch's CPU cumsum accumulates fp32 inputs in double, so this reproduces its
+// fp32 outputs exactly.
+template <int L>
+__device__ __forceinline__ double seg_scan_f64(double x) {
+    x += shr_f64<0x111>(x);
+    x += shr_f64<0x112>(x);
+    x += shr_f64<0x114>(x);
+    x += shr_f64<0x118>(x);
+    if (L >= 32) x += dpp_f64<0x142, 0xA>(x);
+    if (L >= 64) x += dpp_f64<0x143, 0xC>(x);
+    return x;
+}
+
+// The same scan over NA independent dims, step-major so the DPP wait states of
+// one dim are filled by the others (explicit ILP across the A dims).
+template <int L, int NA>
+__device__ __forceinline__ void seg_scan_f64_multi(double (&x)[NA]) {
+    double y[NA];
+#define MPPI_SCAN_STEP(CALL)                                  \
+    _Pragma("unroll") for (int a = 0; a < NA; ++a) y[a] = CALL; \
+    _Pragma("unroll") for (int a = 0; a < NA; ++a) x[a] += y[a];
+    MPPI_SCAN_STEP((shr_f64<0x111>(x[a])))
+    MPPI_SCAN_STEP((shr_f64<0x112>(x[a])))
+    MPPI_SCAN_STEP((shr_f64<0x114>(x[a])))
+    MPPI_SCAN_STEP((shr_f64<0x118>(x[a])))
+    if (L >= 32) { MPPI_SCAN_STEP((dpp_f64<0x142, 0xA>(x[a]))) }
+    if (L >= 64) { MPPI_SCAN_STEP((dpp_f64<0x143, 0xC>(x[a]))) }
+#undef MPPI_SCAN_STEP
+}
+
+// Inclusive fp32 segment sum (cost reduction; order-insensitive at tolerance).
+template <int L>
+__device__ __forceinline__ float seg_scan_f32(float x) {
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xF, 0xF, true));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xF, 0xF, true));
+    if (L >= 32) x += dpp_f32<0x142, 0xA>(x);
+    if (L >= 64) x += dpp_f32<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ float read_lane_f32(float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// Value of segment s's lane l, as a wave-uniform (scalar) quantity.
+template <int R>
+__device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L) {
+    float r = read_lane_f32(x, l_in_seg);
+#pragma unroll
+    for (int s = 1; s < R; ++s) r = (sub == s) ? read_lane_f32(x, s * L + l_in_seg) : r;
+    return r;
+}
+
+template <int MODEL, int NA, int NCH, int LSEG, bool F64>
+__global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
+    constexpr int R = 64 / LSEG;
+    constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
+    constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    // The whole parameter block (scalars, Sigma diagonal, vehicle-0 constants,
+    // joint table) is copied into LDS by all threads in ONE round trip: kernel
+    // arguments are fresh memory every launch, and scattered scalar loads of
+    // them (rematerialised under SGPR pressure) cost a memory round trip each.
+    __shared__ DevParams ps;
+    __shared__ VehicleConst vcv;
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
-    const int L = p.L, H = p.H, K = p.K;
-    const int sub = lane / L, t0 = lane & (L - 1);
-    const VehicleConst& vc = p.vc[v];
-    const bool f64 = (MODEL == MPPI_MODEL_ARM) && p.state_f64;
-
-    // ---- LDS: u_prev tile (H x A) of this vehicle, then wave partials
+    const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
+    STAMP(0);
+    {
+        const int* src = (const int*)&pk;
+        int* dst = (int*)&ps;
+        for (int i = tid; i < (int)(sizeof(DevParams) / 4); i += blockDim.x) dst[i] = src[i];
+        if (pk.V > 1) {
+            const int* vs = (const int*)(pk.vc + v);
+            for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
+        }
+    }
     float* u_lds = smem;
-    const int HA = H * NA;
-    for (int i = tid; i < HA; i += blockDim.x) u_lds[i] = p.u_prev[(size_t)v * HA + i];
-    __syncthreads();
+    const int HA = pk.H * NA;
+    for (int i = tid; i < HA; i += blockDim.x) u_lds[i] = pk.u_prev[(size_t)v * HA + i];
+    // the first group's standard normals overlap the loads above
+    float z0[NCH][NA];
+    if (pk.noise_mode != MPPI_NOISE_INJECTED) {
+        const int64_t kg = pk.k_offset + (int64_t)(blockIdx.x * nw + wid) * R + sub;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+            draw_normals<NA>(z0[c], (uint32_t)kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, pk.step_ctr, pk.seed_lo,
+                             pk.seed_hi);
+    }
+    lds_barrier();
+    const DevParams& p = ps;
+    const VehicleConst& vc = (pk.V == 1) ? ps.vc0 : vcv;
+    const JointDev* jnt = ps.joints;
+    const float* sdiag = ps.sdiag;
+    const int H = pk.H, K = pk.K;
+    STAMP(1);
 
-    const uint32_t step = p.step[0];
     float acc[NCH][NA];
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int a = 0; a < NA; ++a) acc[c][a] = 0.0f;
-    float rho_w = INFINITY, eta_w = 0.0f, eta2_w = 0.0f;
-    int nan_w = 0;
+    float rho_w = INFINITY, eta_w = 0.0f, eta2_w = 0.0f;   // wave-uniform
+    bool nan_w = false;
 
     for (int it = 0; it < p.iters; ++it) {
+        // Launder the loop-invariant scalars through empty asm: keeps the compiler
+        // from hoisting the Philox key schedule, the 19 trajectory-plane offsets and
+        // the LDS constants out of the group loop (SGPR pressure -> spills).
+        asm volatile("" ::: "memory");
+        uint32_t seed_lo = pk.seed_lo, seed_hi = pk.seed_hi;
+        int plane_i = K * H;
+        float* traj_base = pk.traj;
+        asm volatile("" : "+s"(seed_lo), "+s"(seed_hi), "+s"(plane_i), "+s"(traj_base));
         const int g = blockIdx.x + it * p.nb;
-        const int k = (g * nw + wid) * p.R + sub;
+        const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
+        const int kc = kval ? k : K - 1;   // clamped: every load stays in bounds
         const int64_t kg = p.k_offset + k;
 
+        // ---- A1/A2: eps = z Sigma (device Philox) or injected; act = u_prev + eps
         float eps[NCH][NA], act[NCH][NA];
-        double posd[NCH][NA];
-        float posf[NCH][NA];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int t = t0 + 64 * c;
             const bool val = kval && t < H;
+            const int tc = (t < H) ? t : H - 1;
             if (p.noise_mode == MPPI_NOISE_INJECTED) {
-                const float* src = p.noise_in + (((size_t)v * K + k) * H + t) * NA;
+                const float* src = p.noise_in + (((size_t)v * K + kc) * H + tc) * NA;
 #pragma unroll
-                for (int a = 0; a < NA; ++a) eps[c][a] = val ? src[a] : 0.0f;
+                for (int a = 0; a < NA; ++a) eps[c][a] = src[a];
             } else {
                 float z[NA];
-                draw_normals<NA>(z, (uint32_t)kg, (uint32_t)t, (uint32_t)v, step, p.seed_lo, p.seed_hi);
+                if (it == 0) {
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) z[a] = z0[c][a];
+                } else {
+                    draw_normals<NA>(z, (uint32_t)kg, (uint32_t)t, (uint32_t)v, p.step_ctr, seed_lo, seed_hi);
+                }
                 if (p.sigma_diag) {
 #pragma unroll
-                    for (int a = 0; a < NA; ++a) eps[c][a] = val ? z[a] * p.sigma[a * NA + a] : 0.0f;
+                    for (int a = 0; a < NA; ++a) eps[c][a] = z[a] * sdiag[a];
                 } else {
 #pragma unroll
                     for (int b = 0; b < NA; ++b) {
                         float e = 0.0f;
 #pragma unroll
                         for (int a = 0; a < NA; ++a) e += z[a] * p.sigma[a * NA + b];
-                        eps[c][b] = val ? e : 0.0f;
+                        eps[c][b] = e;
                     }
                 }
             }
 #pragma unroll
-            for (int a = 0; a < NA; ++a) act[c][a] = val ? u_lds[t * NA + a] + eps[c][a] : 0.0f;
+            for (int a = 0; a < NA; ++a) {
+                eps[c][a] = val ? eps[c][a] : 0.0f;
+                act[c][a] = val ? u_lds[tc * NA + a] + eps[c][a] : 0.0f;
+            }
             if (p.store_noise && val) {
                 float* dst = p.noise_out + (((size_t)v * K + k) * H + t) * NA;
 #pragma unroll
                 for (int a = 0; a < NA; ++a) dst[a] = eps[c][a];
             }
         }
+        if (it == 0) STAMP(2);
 
-        // ---- double integrator (standard_normal_noise.py:41-48): two fp64
-        //      segment scans per dim; roundings placed where torch rounds.
+        // ---- A3: double integrator (standard_normal_noise.py:41-48), roundings
+        //      where torch rounds; fp32 state -> fp32 positions, fp64 state
+        //      (update_joint of float64 arrays) -> fp64 positions.
+        float posf[NCH][NA];
+        double posd[NCH][F64 ? NA : 1];
         {
 #pragma clang fp contract(off)
+            double carry1[NA], carry2[NA], lastv_d[NA];
+            float lastv_f[NA];
 #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                double carry1 = 0.0, carry2 = 0.0;
-                double last_vel_d = 0.0;
-                float last_vel_f = 0.0f;
+            for (int a = 0; a < NA; ++a) { carry1[a] = 0.0; carry2[a] = 0.0; lastv_d[a] = 0.0; lastv_f[a] = 0.0f; }
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) {
-                    const float s1 = act[c][a] * p.dt;
-                    double c1 = seg_scan((double)s1, L) + carry1;
-                    if (NCH > 1) carry1 = read_lane_f64(c1, 63);
-                    const float c1f = (float)c1;
-                    float dqf = 0.0f;
-                    double dqd = 0.0;
+            for (int c = 0; c < NCH; ++c) {
+                double c1[NA], c2[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) c1[a] = (double)(act[c][a] * p.dt);
+                seg_scan_f64_multi<LSEG, NA>(c1);
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    c1[a] += carry1[a];
+                    if (NCH > 1) carry1[a] = read_lane_f64(c1[a], 63);
+                    const float c1f = (float)c1[a];
                     const float h2 = (0.5f * act[c][a]) * p.dt2;
-                    if (!f64) {
+                    if (!F64) {
                         const float velf = c1f + vc.vel0f[a];
                         float prev = dpp_f32<0x138, 0xF>(velf);     // wave_shr:1
-                        if (t0 == 0) prev = (c == 0) ? vc.vel0f[a] : last_vel_f;
-                        if (NCH > 1) last_vel_f = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(velf), 63));
-                        dqf = prev * p.dt + h2;
-                        dqd = (double)dqf;
+                        if (t0 == 0) prev = (c == 0) ? vc.vel0f[a] : lastv_f[a];
+                        if (NCH > 1) lastv_f[a] = read_lane_f32(velf, 63);
+                        c2[a] = (double)(prev * p.dt + h2);
                     } else {
                         const double vel = (double)c1f + vc.vel0[a];
                         double prev = dpp_f64<0x138, 0xF>(vel);
-                        if (t0 == 0) prev = (c == 0) ? vc.vel0[a] : last_vel_d;
-                        if (NCH > 1) last_vel_d = read_lane_f64(vel, 63);
-                        dqd = prev * p.dt_d + (double)h2;
+                        if (t0 == 0) prev = (c == 0) ? vc.vel0[a] : lastv_d[a];
+                        if (NCH > 1) lastv_d[a] = read_lane_f64(vel, 63);
+                        c2[a] = prev * p.dt_d + (double)h2;
                     }
-                    double c2 = seg_scan(dqd, L) + carry2;
-                    if (NCH > 1) carry2 = read_lane_f64(c2, 63);
-                    if (!f64) {
-                        posf[c][a] = (float)c2 + vc.pos0f[a];
-                        posd[c][a] = (double)posf[c][a];
+                }
+                seg_scan_f64_multi<LSEG, NA>(c2);
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    c2[a] += carry2[a];
+                    if (NCH > 1) carry2[a] = read_lane_f64(c2[a], 63);
+                    if (!F64) {
+                        posf[c][a] = (float)c2[a] + vc.pos0f[a];
                     } else {
-                        posd[c][a] = c2 + vc.pos0[a];
+                        posd[c][a] = c2[a] + vc.pos0[a];
                         posf[c][a] = (float)posd[c][a];
                     }
                 }
             }
         }
+        if (it == 0) STAMP(3);
 
-        // ---- per-(k,t) model: FK + cost, trajectory planes
-        float xs[NCH];   // per-t cost term
+        // ---- A4-A10: FK + per-step cost, trajectory planes
+        float xs[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int t = t0 + 64 * c;
             const bool val = kval && t < H;
             const bool term = (t == H - 1);
             float x;
+            const size_t plane = (size_t)plane_i;
+            float* tdst = traj_base + ((size_t)v * p.C * K + k) * H + t;
             if (MODEL == MPPI_MODEL_DRONE) {
                 const float dx = posf[c][0] - vc.tpos[0], dy = posf[c][1] - vc.tpos[1],
                             dz = posf[c][2] - vc.tpos[2];
                 x = dx * dx + dy * dy + dz * dz;
                 if (p.store_traj && val) {
-                    float* dst = p.traj + ((size_t)v * p.C * K + k) * H + t;
-                    const size_t plane = (size_t)K * H;
-                    dst[0] = posf[c][0]; dst[plane] = posf[c][1]; dst[2 * plane] = posf[c][2];
+                    tdst[0] = posf[c][0]; tdst[plane] = posf[c][1]; tdst[2 * plane] = posf[c][2];
                 }
             } else {
-                Mat34 T;
-                if (MODEL == MPPI_MODEL_ARM) {
+                Mat34 T;   // base (times the folded leading fixed joints)
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) T.m[i] = vc.base[i];
-                } else {   // whole-body: [R(rpy) | p_drone(k,t)]
-#pragma unroll
-                    for (int i = 0; i < 12; ++i) T.m[i] = vc.base[i];
-                    T.m[3] = posf[c][0]; T.m[7] = posf[c][1]; T.m[11] = posf[c][2];
+                for (int i = 0; i < 12; ++i) T.m[i] = vc.base[i];
+                if (MODEL == MPPI_MODEL_WHOLEBODY) {   // [R(rpy) | p_drone(k,t)] * M_fixed
+                    T.m[3] += posf[c][0]; T.m[7] += posf[c][1]; T.m[11] += posf[c][2];
                 }
-                for (int jn = 0; jn < p.nj; ++jn) {
-                    const JointDev& J = p.joints[jn];
-                    mul_affine(T, J.O);
-                    if (J.type == MPPI_JOINT_FIXED) continue;
-                    // select the joint coordinate (q_index is wave-uniform)
-                    double qd = 0.0; float qf = 0.0f;
+                if (p.chain_fast) {   // nq revolute-z joints, q_index = 0..nq-1 in order
 #pragma unroll
-                    for (int a = 0; a < NA - (MODEL == MPPI_MODEL_WHOLEBODY ? 3 : 0); ++a)
-                        if (a == J.q_index) {
-                            qd = posd[c][a + (MODEL == MPPI_MODEL_WHOLEBODY ? 3 : 0)];
-                            qf = posf[c][a + (MODEL == MPPI_MODEL_WHOLEBODY ? 3 : 0)];
-                        }
-                    if (J.type == MPPI_JOINT_REVOLUTE) {
+                    for (int j = 0; j < NQ; ++j) {
+                        const JointDev& J = jnt[p.j0 + j];
+                        mul_affine(T, J.O);
                         float s, cc;
-                        joint_sincos(qd, qf, f64, s, cc);
-                        mul_revolute(T, J, cc, s);
-                    } else {
-                        mul_prismatic(T, J, qf);
+                        sincos_joint(F64 ? posd[c][QOFF + j] : (double)posf[c][QOFF + j], s, cc);
+                        const float omc = 1.0f - cc, r22 = cc + omc;
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            const float a0 = T.m[4 * i], a1 = T.m[4 * i + 1];
+                            T.m[4 * i] = a0 * cc + a1 * s;
+                            T.m[4 * i + 1] = a1 * cc - a0 * s;
+                            T.m[4 * i + 2] = T.m[4 * i + 2] * r22;
+                        }
+                    }
+                } else {
+                    for (int jn = p.j0; jn < p.nj; ++jn) {
+                        const JointDev& J = jnt[jn];
+                        mul_affine(T, J.O);
+                        if (J.type == MPPI_JOINT_FIXED) continue;
+                        double qd = 0.0;
+                        float qf = 0.0f;
+#pragma unroll
+                        for (int a = 0; a < NQ; ++a)
+                            if (a == J.q_index) {
+                                qd = F64 ? posd[c][QOFF + a] : 0.0;
+                                qf = posf[c][QOFF + a];
+                            }
+                        if (J.type == MPPI_JOINT_REVOLUTE) {
+                            float s, cc;
+                            sincos_joint(F64 ? qd : (double)qf, s, cc);
+                            mul_revolute(T, J, cc, s);
+                        } else {
+                            mul_prismatic(T, J, qf);
+                        }
                     }
                 }
                 x = term ? pose_cost(T, vc, p.w_tp, p.w_to) : pose_cost(T, vc, p.w_sp, p.w_so);
                 if (p.store_traj && val) {
-                    const size_t plane = (size_t)K * H;
-                    float* dst = p.traj + ((size_t)v * p.C * K + k) * H + t;
 #pragma unroll
-                    for (int a = 0; a < NA; ++a) dst[a * plane] = posf[c][a];
+                    for (int a = 0; a < NA; ++a) tdst[a * plane] = posf[c][a];
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) dst[(NA + i) * plane] = T.m[i];
+                    for (int i = 0; i < 12; ++i) tdst[(NA + i) * plane] = T.m[i];
                 }
             }
             xs[c] = val ? x : 0.0f;
         }
+        if (it == 0) STAMP(4);
 
-        // ---- S_k = fl(ws * sum_{t<H-1} x_t) + fl(wt * x_{H-1})  (segment reduction)
-        double stage = 0.0;
+        // ---- S_k = fl(ws * sum_{t<H-1} x_t) + fl(wt * x_{H-1}) per segment (wave-uniform picks)
+        float st = 0.0f;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int t = t0 + 64 * c;
-            stage += (t < H - 1) ? (double)xs[c] : 0.0;
-        }
-        stage = seg_scan(stage, L);
-        const int seg_base = lane & ~(L - 1);
-        stage = __shfl(stage, seg_base + L - 1);
-        float xterm = 0.0f;
+        for (int c = 0; c < NCH; ++c) st += (t0 + 64 * c < H - 1) ? xs[c] : 0.0f;
+        st = seg_scan_f32<LSEG>(st);
+        float xt = 0.0f;
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
-            if (c == (H - 1) / 64) xterm = __shfl(xs[c], seg_base + ((H - 1) & 63));
-        float S;
-        if (MODEL == MPPI_MODEL_DRONE) S = (p.w_sp * (float)stage) + (p.w_tp * xterm);
-        else S = (float)stage + xterm;
-        if (!kval) S = INFINITY;
-        if (kval && t0 == 0) p.S[(size_t)v * K + k] = S;
+            if (c == (H - 1) / 64) xt = xs[c];
+        float S_seg[R];
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const int ks = (g * nw + wid) * R + s;
+            const float stage = read_lane_f32(st, s * LSEG + LSEG - 1);
+            const float term = read_lane_f32(xt, s * LSEG + ((H - 1) & 63));
+            float S = (MODEL == MPPI_MODEL_DRONE) ? (p.w_sp * stage) + (p.w_tp * term) : stage + term;
+            S_seg[s] = (ks < K) ? S : INFINITY;
+        }
+        float S_mine = S_seg[0];
+#pragma unroll
+        for (int s = 1; s < R; ++s) S_mine = (sub == s) ? S_seg[s] : S_mine;
+        if (kval && t0 == 0) p.S[(size_t)v * K + k] = S_mine;
 
-        // ---- online softmin (mppi.py:184-188) across this wave's rollouts
-        const bool bad = kval && (S != S);
-        nan_w |= __any(bad) ? 1 : 0;
-        float m = bad ? INFINITY : S;
-        for (int o = L; o < 64; o <<= 1) m = fminf(m, __shfl_xor(m, o));
+        // ---- online softmin (mppi.py:184-188) over this wave's rollouts (scalar bookkeeping)
+        float m = INFINITY;
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const bool bad = S_seg[s] != S_seg[s];
+            nan_w |= bad;
+            if (!bad) m = fminf(m, S_seg[s]);
+        }
         if (m < INFINITY) {
             const float rn = fminf(rho_w, m);
             const float f = (rho_w == INFINITY) ? 0.0f : __expf(p.coef * (rho_w - rn));
-            const float e = (bad || !kval) ? 0.0f : __expf(p.coef * (S - rn));
-            float es = (t0 == 0) ? e : 0.0f, e2 = es * es;
-            for (int o = 1; o < 64; o <<= 1) { es += __shfl_xor(es, o); e2 += __shfl_xor(e2, o); }
+            float es = 0.0f, e2 = 0.0f;
+#pragma unroll
+            for (int s = 0; s < R; ++s) {
+                const float e = (S_seg[s] < INFINITY) ? __expf(p.coef * (S_seg[s] - rn)) : 0.0f;
+                es += e;
+                e2 += e * e;
+            }
             eta_w = eta_w * f + es;
             eta2_w = eta2_w * f * f + e2;
+            const float e_mine = (kval && !(S_mine != S_mine)) ? __expf(p.coef * (S_mine - rn)) : 0.0f;
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
-                for (int a = 0; a < NA; ++a) acc[c][a] = acc[c][a] * f + e * eps[c][a];
+                for (int a = 0; a < NA; ++a) acc[c][a] = acc[c][a] * f + e_mine * eps[c][a];
             rho_w = rn;
         }
     }
+    STAMP(5);
 
-    // ---- fold the R segments of the wave (same rho_w): lanes t0 hold totals
+    // ---- cross-wave combine in LDS -> one partial record per block
+    //      LDS: [nw][4 + NCH*64*NA]; every lane (all R segments) deposits acc
+    float* wsh = smem + ((HA + 3) & ~3);
+    const int wstride = 4 + NCH * 64 * NA;
+    float* mine = wsh + wid * wstride;
+    if (lane == 0) { mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f; }
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int a = 0; a < NA; ++a)
-            for (int o = L; o < 64; o <<= 1) acc[c][a] += __shfl_xor(acc[c][a], o);
-
-    // ---- cross-wave combine in LDS -> one partial record per block
-    float* wsh = smem + ((HA + 3) & ~3);          // [nw][4 + NCH*64*NA]
-    const int wstride = 4 + NCH * 64 * NA;
-    float* mine = wsh + wid * wstride;
-    if (lane == 0) { mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = (float)nan_w; }
-    if (sub == 0) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-#pragma unroll
-            for (int a = 0; a < NA; ++a) mine[4 + (c * 64 + t0) * NA + a] = acc[c][a];
-    }
-    __syncthreads();
+        for (int a = 0; a < NA; ++a) mine[4 + (c * 64 + lane) * NA + a] = acc[c][a];
+    lds_barrier();
+    STAMP(6);
+    __shared__ float fw[16];
     float rho_b = INFINITY;
     for (int w = 0; w < nw; ++w) rho_b = fminf(rho_b, wsh[w * wstride]);
+    if (tid < nw) {
+        const float rw = wsh[tid * wstride];
+        fw[tid] = (rw == INFINITY) ? 0.0f : __expf(p.coef * (rw - rho_b));
+    }
+    lds_barrier();
     float* rec = p.part + ((size_t)v * p.nb + blockIdx.x) * p.P;
     if (tid == 0) {
         float eta = 0.0f, eta2 = 0.0f, nanf = 0.0f;
         for (int w = 0; w < nw; ++w) {
-            const float rw = wsh[w * wstride];
-            const float f = (rw == INFINITY) ? 0.0f : __expf(p.coef * (rw - rho_b));
-            eta += f * wsh[w * wstride + 1];
-            eta2 += f * f * wsh[w * wstride + 2];
+            eta += fw[w] * wsh[w * wstride + 1];
+            eta2 += fw[w] * fw[w] * wsh[w * wstride + 2];
             nanf = fmaxf(nanf, wsh[w * wstride + 3]);
         }
         rec[0] = rho_b; rec[1] = eta; rec[2] = eta2; rec[3] = nanf;
     }
-    // record body a-major: N[a*H + t]
+    // record body a-major: N[a*H + t] = sum_w f_w sum_segments acc_w[seg*L + t]
     for (int i = tid; i < HA; i += blockDim.x) {
         const int a = i / H, t = i - a * H;
         const int c = t >> 6, tl = t & 63;
         float s = 0.0f;
-        for (int w = 0; w < nw; ++w) {
-            const float rw = wsh[w * wstride];
-            const float f = (rw == INFINITY) ? 0.0f : __expf(p.coef * (rw - rho_b));
-            s += f * wsh[w * wstride + 4 + (c * 64 + tl) * NA + a];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            if (w < nw) {
+                float sw = 0.0f;
+#pragma unroll
+                for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
+                s += fw[w] * sw;
+            }
         }
         rec[kHdr + i] = s;
     }
+    STAMP(7);
 }
 
 // =============================================================================
 // k_finalize: grid (A, V); block a owns action dim a of vehicle v.
+//   1. rho = min_r rho_r                     (record headers)
+//   2. f_r = exp(-(rho_r - rho)/lambda); eta = sum f_r eta_r   (fp64 sums)
+//   3. N[t] = sum_r f_r N_r[a][t]            (16-byte loads, all in flight)
+//   PACK: write (rho, eta, eta2, nan | N) into the shard's exchange slot.
+//   FINAL: w_eps = N/eta, SavGol (symmetric pad), u += w_eps, outputs written
+//          straight into mapped pinned host memory (no D2H copy).
 // =============================================================================
 constexpr int kFinThreads = 256;
 constexpr int kMaxRec = 4096;
+constexpr int kNPT = 8;
 
-__global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams p) {
-    __shared__ float f_lds[kMaxRec];
-    __shared__ double red[kFinThreads];
-    __shared__ float nsum[kFinThreads];
+// DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
+// result lands in lane 63 and is broadcast with readlane (no LDS round trips).
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_id(float x, float id) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(x), CTRL, RM, 0xF, false));
+}
+__device__ __forceinline__ float wave_min(float x) {
+    x = fminf(x, dpp_id<0x111, 0xF>(x, INFINITY));
+    x = fminf(x, dpp_id<0x112, 0xF>(x, INFINITY));
+    x = fminf(x, dpp_id<0x114, 0xF>(x, INFINITY));
+    x = fminf(x, dpp_id<0x118, 0xF>(x, INFINITY));
+    x = fminf(x, dpp_id<0x142, 0xA>(x, INFINITY));
+    x = fminf(x, dpp_id<0x143, 0xC>(x, INFINITY));
+    return read_lane_f32(x, 63);
+}
+__device__ __forceinline__ float wave_max(float x) {
+    x = fmaxf(x, dpp_id<0x111, 0xF>(x, -INFINITY));
+    x = fmaxf(x, dpp_id<0x112, 0xF>(x, -INFINITY));
+    x = fmaxf(x, dpp_id<0x114, 0xF>(x, -INFINITY));
+    x = fmaxf(x, dpp_id<0x118, 0xF>(x, -INFINITY));
+    x = fmaxf(x, dpp_id<0x142, 0xA>(x, -INFINITY));
+    x = fmaxf(x, dpp_id<0x143, 0xC>(x, -INFINITY));
+    return read_lane_f32(x, 63);
+}
+__device__ __forceinline__ double wave_sum_f64(double x) {
+    x += shr_f64<0x111>(x);
+    x += shr_f64<0x112>(x);
+    x += shr_f64<0x114>(x);
+    x += shr_f64<0x118>(x);
+    x += dpp_f64<0x142, 0xA>(x);
+    x += dpp_f64<0x143, 0xC>(x);
+    return read_lane_f64(x, 63);
+}
+
+#ifdef MPPI_STAMPS
+#define FSTAMP(i)                                                                    \
+    do {                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+        if (p.stamps && threadIdx.x == 0)                                            \
+            p.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps + (i)] = \
+                __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+    } while (0)
+#else
+#define FSTAMP(i) do { } while (0)
+#endif
+
+__global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
+    constexpr int NWV = kFinThreads / 64;
+    __shared__ FinParams ps;   // one-round-trip copy of the kernel arguments (see k_rollout)
+    {
+        const int* src = (const int*)&pk;
+        for (int i = threadIdx.x; i < (int)(sizeof(FinParams) / 4); i += kFinThreads) ((int*)&ps)[i] = src[i];
+    }
+    lds_barrier();
+    const FinParams& p = ps;
+    __shared__ float4 part4[kFinThreads];
     __shared__ float wcol[MPPI_MAX_HORIZON + 2 * kMaxW];
-    __shared__ float s_rho, s_nan;
-    __shared__ double s_eta, s_eta2;
+    __shared__ float shm[2 * NWV];
+    __shared__ double shd[2 * NWV];
     const int a = blockIdx.x, v = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    FSTAMP(0);
     const int H = p.H, n = p.nrec;
     const float* recs = p.rec + (size_t)v * p.rec_vstride;
+    const size_t rs = (size_t)p.rec_rstride;
 
-    // 1. rho = min over records; NaN flag
-    float m = INFINITY, nanf = 0.0f;
-    for (int r = tid; r < n; r += kFinThreads) {
-        m = fminf(m, recs[(size_t)r * p.rec_rstride]);
-        nanf = fmaxf(nanf, recs[(size_t)r * p.rec_rstride + 3]);
-    }
-    red[tid] = m;
-    nsum[tid] = nanf;
-    __syncthreads();
-    for (int s = kFinThreads / 2; s > 0; s >>= 1) {
-        if (tid < s) { red[tid] = fmin(red[tid], red[tid + s]); nsum[tid] = fmaxf(nsum[tid], nsum[tid + s]); }
-        __syncthreads();
-    }
-    if (tid == 0) { s_rho = (float)red[0]; s_nan = nsum[0]; }
-    __syncthreads();
-    const float rho = s_rho;
-
-    // 2. rescale factors and normalisers (fp64 accumulation, fixed order)
+    // Thread (g, q): column chunk q (4 consecutive t when H % 4 == 0, else 1 t)
+    // of records g, g + rows, ...  Headers and column data are loaded in one
+    // pass (kNPT records per thread, all loads in flight) when n <= rows*kNPT.
+    const bool vec = (H & 3) == 0;
+    const int tpr = vec ? (H >> 2) : H;
+    const int rows = kFinThreads / tpr;
+    const int g = tid / tpr, q = tid - g * tpr;
+    const bool active = g < rows;
+    const float* col = recs + kHdr + (size_t)a * H;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     double eta = 0.0, eta2 = 0.0;
-    for (int r = tid; r < n; r += kFinThreads) {
-        const float* rc = recs + (size_t)r * p.rec_rstride;
-        const float f = (rc[0] == INFINITY) ? 0.0f : __expf(p.coef * (rc[0] - rho));
-        f_lds[r] = f;
-        eta += (double)f * rc[1];
-        eta2 += (double)f * f * rc[2];
-    }
-    red[tid] = eta;
-    __syncthreads();
-    for (int s = kFinThreads / 2; s > 0; s >>= 1) { if (tid < s) red[tid] += red[tid + s]; __syncthreads(); }
-    if (tid == 0) s_eta = red[0];
-    __syncthreads();
-    red[tid] = eta2;
-    __syncthreads();
-    for (int s = kFinThreads / 2; s > 0; s >>= 1) { if (tid < s) red[tid] += red[tid + s]; __syncthreads(); }
-    if (tid == 0) s_eta2 = red[0];
-    __syncthreads();
-
-    // 3. N[t] = sum_r f_r N_r[a][t]: thread = (t, record group)
-    const int groups = kFinThreads / H > 0 ? kFinThreads / H : 1;
-    float acc_t[MPPI_MAX_HORIZON / kFinThreads + 1];
-    const int tpt = (H + kFinThreads - 1) / kFinThreads;   // t per thread when H > threads
-    for (int i = 0; i < tpt; ++i) acc_t[i] = 0.0f;
-    if (H <= kFinThreads) {
-        const int t = tid % H, gidx = tid / H;
-        float s = 0.0f;
-        if (gidx < groups)
-            for (int r = gidx; r < n; r += groups)
-                s += f_lds[r] * recs[(size_t)r * p.rec_rstride + kHdr + a * H + t];
-        nsum[tid] = s;
-        __syncthreads();
-        if (tid < H) {
-            float tot = 0.0f;
-            for (int g = 0; g < groups; ++g) tot += nsum[g * H + tid];
-            wcol[kMaxW + tid] = tot;
+    float rho, nanflag;
+    auto block_minmax = [&](float m, float nf) {
+        m = wave_min(m);
+        nf = wave_max(nf);
+        if (lane == 0) { shm[wv] = m; shm[NWV + wv] = nf; }
+        lds_barrier();
+        rho = shm[0]; nanflag = shm[NWV];
+#pragma unroll
+        for (int i = 1; i < NWV; ++i) { rho = fminf(rho, shm[i]); nanflag = fmaxf(nanflag, shm[NWV + i]); }
+    };
+    if (p.dbg & 1) {          // diagnostic: skip the record loads
+        rho = 0.0f; nanflag = 0.0f;
+    } else if (n <= rows * kNPT) {
+        float4 hd[kNPT], xv[kNPT];
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) {
+            const int r = g + i * rows;
+            const bool ok = active && r < n;
+            const size_t ro = (size_t)(ok ? r : 0) * rs;
+            hd[i] = *reinterpret_cast<const float4*>(recs + ro);
+            if (vec) xv[i] = *reinterpret_cast<const float4*>(col + ro + 4 * q);
+            else xv[i] = make_float4(col[ro + q], 0.f, 0.f, 0.f);
+            if (!ok) { hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f); xv[i] = make_float4(0.f, 0.f, 0.f, 0.f); }
+        }
+        float m = INFINITY, nf = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nf = fmaxf(nf, hd[i].w); }
+        FSTAMP(1);
+        block_minmax(m, nf);
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) {
+            const float f = (hd[i].x == INFINITY) ? 0.0f : __expf(p.coef * (hd[i].x - rho));
+            acc.x = fmaf(f, xv[i].x, acc.x); acc.y = fmaf(f, xv[i].y, acc.y);
+            acc.z = fmaf(f, xv[i].z, acc.z); acc.w = fmaf(f, xv[i].w, acc.w);
+            if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
         }
     } else {
-        for (int i = 0; i < tpt; ++i) {
-            const int t = tid + i * kFinThreads;
-            if (t >= H) break;
-            float s = 0.0f;
-            for (int r = 0; r < n; ++r) s += f_lds[r] * recs[(size_t)r * p.rec_rstride + kHdr + a * H + t];
-            wcol[kMaxW + t] = s;
+        float m = INFINITY, nf = 0.0f;
+        for (int r = tid; r < n; r += kFinThreads) {
+            m = fminf(m, recs[r * rs]);
+            nf = fmaxf(nf, recs[r * rs + 3]);
+        }
+        FSTAMP(1);
+        block_minmax(m, nf);
+        if (active) {
+#pragma unroll 4
+            for (int r = g; r < n; r += rows) {
+                const float4 hd = *reinterpret_cast<const float4*>(recs + r * rs);
+                const float f = (hd.x == INFINITY) ? 0.0f : __expf(p.coef * (hd.x - rho));
+                float4 x;
+                if (vec) x = *reinterpret_cast<const float4*>(col + r * rs + 4 * q);
+                else x = make_float4(col[r * rs + q], 0.f, 0.f, 0.f);
+                acc.x = fmaf(f, x.x, acc.x); acc.y = fmaf(f, x.y, acc.y);
+                acc.z = fmaf(f, x.z, acc.z); acc.w = fmaf(f, x.w, acc.w);
+                if (q == 0) { eta += (double)f * hd.y; eta2 += (double)f * f * hd.z; }
+            }
         }
     }
-    __syncthreads();
+    FSTAMP(2);
+    // eta / eta2: DPP wave sums, then the NWV wave totals
+    {
+        const double e1 = wave_sum_f64(eta), e2 = wave_sum_f64(eta2);
+        if (lane == 0) { shd[wv] = e1; shd[NWV + wv] = e2; }
+    }
+    // column partials: log-step tree over g in LDS (no serial dependent chains)
+    part4[tid] = acc;
+    lds_barrier();
+    eta = shd[0]; eta2 = shd[NWV];
+#pragma unroll
+    for (int i = 1; i < NWV; ++i) { eta += shd[i]; eta2 += shd[NWV + i]; }
+    FSTAMP(3);
+    int span = 1;
+    while (span < rows) span <<= 1;
+    for (int s = span >> 1; s > 0; s >>= 1) {
+        if (active && g < s && g + s < rows) {
+            const float4 o = part4[(g + s) * tpr + q];
+            float4 x = part4[tid];
+            x.x += o.x; x.y += o.y; x.z += o.z; x.w += o.w;
+            part4[tid] = x;
+        }
+        lds_barrier();
+    }
+    for (int t = tid; t < H; t += kFinThreads) {
+        const float4 x = part4[vec ? (t >> 2) : t];
+        const int l4 = vec ? (t & 3) : 0;
+        wcol[kMaxW + t] = l4 == 0 ? x.x : l4 == 1 ? x.y : l4 == 2 ? x.z : x.w;
+    }
+    lds_barrier();
+    FSTAMP(4);
 
     if (p.mode == 1) {   // PACK into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
         if (a == 0 && tid == 0) {
-            dst[0] = rho; dst[1] = (float)s_eta; dst[2] = (float)s_eta2; dst[3] = s_nan;
+            dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanflag;
         }
         for (int t = tid; t < H; t += kFinThreads) dst[kHdr + a * H + t] = wcol[kMaxW + t];
         return;
     }
+    if (p.dbg & 2) return;    // diagnostic: stop after the reduction
 
-    // 4. FINAL: w_eps = N / eta; SavGol (symmetric pad); u += w_eps; outputs
-    const float etaf = (s_nan > 0.0f) ? NAN : (float)s_eta;
-    for (int t = tid; t < H; t += kFinThreads) {
-        const float w = wcol[kMaxW + t] / etaf;
-        wcol[kMaxW + t] = w;
-        if (p.wraw) p.wraw[((size_t)v * H + t) * p.A + a] = w;
-    }
-    __syncthreads();
+    // FINAL: w_eps = N/eta, SavGol (symmetric pad, svg_filter.py:58), u += w_eps
+    const float etaf = (nanflag > 0.0f) ? NAN : (float)eta;
+    float* up = p.u_prev + (size_t)v * H * p.A;
+    const float uold0 = up[a];
     const int hf = p.half;
+    float wv_t = 0.0f;
+    if (tid < H) {
+        wv_t = wcol[kMaxW + tid] / etaf;
+        wcol[kMaxW + tid] = wv_t;
+        if (p.wraw) p.wraw[((size_t)v * H + tid) * p.A + a] = wv_t;
+    }
+    lds_barrier();
     if (tid < hf) {   // [d_{h-1} .. d_0 | d | d_{N-1} .. d_{N-h}]
         wcol[kMaxW - 1 - tid] = wcol[kMaxW + tid];
         wcol[kMaxW + H + tid] = wcol[kMaxW + H - 1 - tid];
     }
-    __syncthreads();
-    float* up = p.u_prev + (size_t)v * H * p.A;
-    const float uold0 = up[a];
-    __syncthreads();
+    lds_barrier();
     for (int t = tid; t < H; t += kFinThreads) {
         float s = 0.0f;
         for (int j = 0; j < p.window; ++j) s += p.sg[j] * wcol[kMaxW - hf + t + j];
         if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * p.A + a] = s;
-        up[t * p.A + a] = up[t * p.A + a] + s;
+        const float un = up[t * p.A + a] + s;
+        up[t * p.A + a] = un;
+        if (t == 0) wcol[0] = un;   // u0 for the output thread
     }
-    __syncthreads();
-    if (tid == 0) {
+    lds_barrier();
+    FSTAMP(5);
+    if (tid == 0 && !(p.dbg & 4)) {
 #pragma clang fp contract(off)
-        const float u0 = up[a];
+        const float u0 = wcol[0];
         p.u0[(size_t)v * p.A + a] = u0;
-        const VehicleConst& vc = p.vc[v];
+        const VehicleConst& vc = (p.V == 1) ? p.vc0 : p.vc[v];
         double* out = p.out + (size_t)v * p.out_dim;
         const bool drone_dim = (p.model == MPPI_MODEL_DRONE) || (p.model == MPPI_MODEL_WHOLEBODY && a < 3);
         if (drone_dim) {   // drone_mppi.py:168-169
@@ -595,15 +902,14 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams p) {
             }
         }
         if (a == 0) {
-            const double e = s_eta, e2 = s_eta2;
             float* st = p.stats + (size_t)v * 4;
             st[0] = rho;
-            st[1] = (float)e;
-            st[2] = (e2 > 0.0) ? (float)(e * e / e2) : 0.0f;
-            st[3] = s_nan;
-            if (v == 0) p.step[0] = p.step[0] + 1u;
+            st[1] = (float)eta;
+            st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
+            st[3] = nanflag;
         }
     }
+    FSTAMP(6);
 }
 
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only
@@ -638,37 +944,38 @@ __global__ void k_philox(uint64_t seed, uint32_t step, int veh, int64_t k0, int 
 // =============================================================================
 // launchers
 // =============================================================================
-template <int MODEL, int NA, int NCH>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64>
 static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
     const int nw = threads / 64;
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + nw * (4 + NCH * 64 * NA)) * sizeof(float);
-    hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
+    hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
     return (int)hipGetLastError();
 }
 
-template <int MODEL, int NA>
-static int dispatch_nch(const DevParams& p, int threads, hipStream_t s) {
-    switch (p.nch) {
-        case 1: return launch_rollout_t<MODEL, NA, 1>(p, threads, s);
-        case 2: return launch_rollout_t<MODEL, NA, 2>(p, threads, s);
-        case 4: return launch_rollout_t<MODEL, NA, 4>(p, threads, s);
-        default: return -1;
-    }
+template <int MODEL, int NA, bool F64>
+static int dispatch_geom(const DevParams& p, int threads, hipStream_t s) {
+    if (p.nch == 1 && p.L == 32) return launch_rollout_t<MODEL, NA, 1, 32, F64>(p, threads, s);
+    if (p.nch == 1 && p.L == 64) return launch_rollout_t<MODEL, NA, 1, 64, F64>(p, threads, s);
+    if (p.nch == 2) return launch_rollout_t<MODEL, NA, 2, 64, F64>(p, threads, s);
+    if (p.nch == 4) return launch_rollout_t<MODEL, NA, 4, 64, F64>(p, threads, s);
+    return -1;
 }
 
 extern "C" int mppi_launch_rollout(const DevParams* p, int threads, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     switch (p->model) {
         case MPPI_MODEL_DRONE:
-            if (p->A == 3) return dispatch_nch<MPPI_MODEL_DRONE, 3>(*p, threads, s);
+            if (p->A == 3) return dispatch_geom<MPPI_MODEL_DRONE, 3, false>(*p, threads, s);
             break;
         case MPPI_MODEL_ARM:
-            if (p->A == 7) return dispatch_nch<MPPI_MODEL_ARM, 7>(*p, threads, s);
-            if (p->A == 6) return dispatch_nch<MPPI_MODEL_ARM, 6>(*p, threads, s);
+            if (p->A == 7) return p->state_f64 ? dispatch_geom<MPPI_MODEL_ARM, 7, true>(*p, threads, s)
+                                               : dispatch_geom<MPPI_MODEL_ARM, 7, false>(*p, threads, s);
+            if (p->A == 6) return p->state_f64 ? dispatch_geom<MPPI_MODEL_ARM, 6, true>(*p, threads, s)
+                                               : dispatch_geom<MPPI_MODEL_ARM, 6, false>(*p, threads, s);
             break;
         case MPPI_MODEL_WHOLEBODY:
-            if (p->A == 10) return dispatch_nch<MPPI_MODEL_WHOLEBODY, 10>(*p, threads, s);
-            if (p->A == 9) return dispatch_nch<MPPI_MODEL_WHOLEBODY, 9>(*p, threads, s);
+            if (p->A == 10) return dispatch_geom<MPPI_MODEL_WHOLEBODY, 10, false>(*p, threads, s);
+            if (p->A == 9) return dispatch_geom<MPPI_MODEL_WHOLEBODY, 9, false>(*p, threads, s);
             break;
     }
     return -1;

@@ -1,0 +1,83 @@
+"""Sample sharding over GPUs: one process per GPU, one all-reduce per step.
+
+SURVEY.md §8e: rollouts are independent until the softmin, so rank g owns the
+global samples [g*K, (g+1)*K) (the device Philox stream is keyed by the global
+sample index, so the noise does not depend on the GPU count).  Each rank folds
+its rollouts into one partial record (rho_g, eta_g, eta2_g, N_g[A*H]) and writes
+it into slot g of a zero-initialised (G, V, P) exchange buffer; ONE
+``all_reduce(SUM)`` over RCCL/xGMI (backend "nccl") then hands every rank all G
+slots (x + 0 is exact, so the sum is a gather), and every rank runs the same
+finalize: rho = min_g rho_g, rescale by exp(-(rho_g - rho)/lambda), SavGol,
+u += w_eps.  The payload is (4 + A*H) floats per vehicle per rank -- 2.6 KB at
+H=64, A=10 -- so the collective is latency-bound; ring bandwidth is irrelevant.
+
+The reference has no distributed code (single process, ``CUDA_VISIBLE_DEVICES='0'``
+at ``mppi.py:31``); there is no reference collective to mirror.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .engine import Engine, make_config
+
+HDR = 4   # partial record header: rho, eta, eta2, nan-flag
+
+
+def all_reduce_slots(buf: torch.Tensor, group=None) -> torch.Tensor:
+    """The single collective of a control step (SUM over a zero-padded slot buffer)."""
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf
+
+
+def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
+    """Host restatement of the finalize combine for a (G, P) slot array -> raw
+    w_eps (H, A).  Used by the CPU (gloo) tests of the exchange protocol; the
+    device path is ``k_finalize`` in mppi_kernels.hip."""
+    rho = slots[:, 0].astype(np.float64)
+    r = rho.min()
+    f = np.exp(-(rho - r) / lam)
+    eta = float((f * slots[:, 1]).sum())
+    N = (f[:, None] * slots[:, HDR:HDR + A * H].astype(np.float64)).sum(0)
+    return (N / eta).reshape(A, H).T
+
+
+class ShardedEngine:
+    """One rank's engine of a sample-sharded MPPI controller."""
+
+    def __init__(self, group=None, exchange: Callable = all_reduce_slots, **engine_kw):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.local = int(os.environ.get("LOCAL_RANK", engine_kw.pop("device", 0)))
+        torch.cuda.set_device(self.local)
+        cfg = make_config(device=self.local, shard_rank=self.rank, shard_count=self.world, **engine_kw)
+        self.engine = Engine(cfg)
+        self.engine.set_stream(torch.cuda.current_stream(self.local).cuda_stream)
+        self._exchange = exchange
+        self.buf: Optional[torch.Tensor] = None
+        if self.world > 1:
+            slot = self.engine.exchange_slot_floats()
+            self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")
+            self.engine.bind_exchange(self.buf.data_ptr())
+
+    def step_async(self, d_noise_ptr: int = 0):
+        """rollout -> (all-reduce) -> finalize, all stream-ordered, no host sync."""
+        self.engine.rollout(d_noise_ptr)
+        if self.world > 1:
+            self._exchange(self.buf, self.group)
+        self.engine.finalize()
+
+    def step(self, state, d_noise_ptr: int = 0):
+        self.engine.set_state(state)
+        self.step_async(d_noise_ptr)
+        return self.engine.read_outputs()
+
+    def __getattr__(self, name):
+        if name == "engine":
+            raise AttributeError(name)
+        return getattr(self.engine, name)

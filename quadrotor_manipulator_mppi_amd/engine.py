@@ -173,6 +173,10 @@ class Engine:
                                              self._stats), "read_outputs")
         return self._out.copy(), self._u0.copy(), self.stats()
 
+    def run_steps(self, n: int):
+        """n asynchronous back-to-back control steps (no host sync)."""
+        capi.check(self._L.mppi_run_steps(self._h, n), "run_steps")
+
     def synchronize(self):
         capi.check(self._L.mppi_synchronize(self._h), "synchronize")
 
