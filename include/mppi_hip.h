@@ -203,6 +203,12 @@ mppi_status mppi_get_weighted_noise(mppi_engine* e, float* raw, float* smoothed)
 mppi_status mppi_enable_timing(mppi_engine* e, int32_t enable);
 mppi_status mppi_get_timing(mppi_engine* e, double* rollout_ms_total, double* finalize_ms_total,
                             int64_t* n_rollout, int64_t* n_finalize);
+/* Average device time of the two kernels measured back to back: n rollout launches
+ * bracketed by one event pair, then n finalize launches bracketed by another (the
+ * per-launch pairs of mppi_enable_timing add ~2-3 us of event overhead each).  The
+ * warm start and step counter are saved and restored, so the controller state is
+ * unchanged.  Single-shard engines with device noise. */
+mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us);
 
 /* Algorithmic HBM bytes one mppi_rollout launch moves. */
 int64_t mppi_rollout_bytes(const mppi_config* cfg);

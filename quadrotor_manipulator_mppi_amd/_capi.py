@@ -89,6 +89,7 @@ PROTOTYPES = {
     "mppi_get_weighted_noise": (_ST, [_P, _F, _F]),
     "mppi_enable_timing": (_ST, [_P, C.c_int32]),
     "mppi_get_timing": (_ST, [_P, _D, _D, _I64, _I64]),
+    "mppi_kernel_timing": (_ST, [_P, C.c_int32, _D, _D]),
     "mppi_rollout_bytes": (C.c_int64, [_CFG]),
     "mppi_joint_origin": (None, [C.POINTER(Joint), _F]),
     "mppi_base_transform": (None, [_D, C.c_int32, _F]),

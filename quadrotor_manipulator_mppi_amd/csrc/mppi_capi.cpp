@@ -263,7 +263,9 @@ struct mppi_engine {
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
     float* d_S = nullptr;
-    float* d_part = nullptr;
+    float* d_hdr = nullptr;     // (V,nb,4) block record headers
+    float* d_rdata = nullptr;   // (V,A,nb,H) block record bodies
+    int fin_ts = 1, fin_tsz = 8;   // finalize t-slices
     unsigned char* d_out = nullptr;   // out doubles | u0 floats | stats floats
     float* d_wraw = nullptr;
     float* d_wsmooth = nullptr;
@@ -392,10 +394,12 @@ mppi_status validate(const mppi_config& c) {
         return fail(MPPI_ERR_INVALID_ARG, "bad sizes V=%d K=%d H=%d", c.n_vehicles, c.n_samples, c.n_horizon);
     if (c.model == MPPI_MODEL_DRONE && c.n_action != 3)
         return fail(MPPI_ERR_INVALID_ARG, "DRONE needs n_action=3");
-    if (c.model == MPPI_MODEL_ARM && c.n_action != 6 && c.n_action != 7)
-        return fail(MPPI_ERR_INVALID_ARG, "ARM supports n_action 6 or 7 (got %d)", c.n_action);
-    if (c.model == MPPI_MODEL_WHOLEBODY && c.n_action != 9 && c.n_action != 10)
-        return fail(MPPI_ERR_INVALID_ARG, "WHOLEBODY supports n_action 9 or 10 (got %d)", c.n_action);
+    if (c.model == MPPI_MODEL_ARM && c.n_action != 7)
+        return fail(MPPI_ERR_INVALID_ARG, "ARM kernels are built for the 7-DoF Kinova chain (n_action 7, got %d)",
+                    c.n_action);
+    if (c.model == MPPI_MODEL_WHOLEBODY && c.n_action != 10)
+        return fail(MPPI_ERR_INVALID_ARG, "WHOLEBODY kernels are built for 3 + 7 dims (n_action 10, got %d)",
+                    c.n_action);
     if (c.model != MPPI_MODEL_DRONE) {
         if (c.n_joints < 1 || c.n_joints > MPPI_MAX_JOINTS)
             return fail(MPPI_ERR_INVALID_ARG, "n_joints=%d", c.n_joints);
@@ -591,7 +595,8 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_u_prev, sizeof(float) * e->V * H * e->A));
     CREATE_TRY(hipMalloc(&e->d_S, sizeof(float) * e->V * e->K));
     CREATE_TRY(hipMalloc(&e->d_w, sizeof(float) * e->V * e->K));
-    CREATE_TRY(hipMalloc(&e->d_part, sizeof(float) * (size_t)e->V * nb * P));
+    CREATE_TRY(hipMalloc(&e->d_hdr, sizeof(float) * (size_t)e->V * nb * 4));
+    CREATE_TRY(hipMalloc(&e->d_rdata, sizeof(float) * (size_t)e->V * e->A * nb * H));
     CREATE_TRY(hipMalloc(&e->d_wraw, sizeof(float) * e->V * H * e->A));
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
     if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * KH * e->C));
@@ -652,13 +657,13 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.w_sp = c.w_stage_pos; p.w_so = c.w_stage_ori; p.w_tp = c.w_term_pos; p.w_to = c.w_term_ori;
     for (int j = 0; j < kMaxJ; ++j) p.joints[j] = jd[j];
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
-    p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.part = e->d_part;
+    p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS
     if (getenv("MPPI_STAMPS")) {
         const size_t nwaves = (size_t)e->V * nb * (e->threads / 64);
         if (hipMalloc(&e->d_stamps, nwaves * kStamps * 8) == hipSuccess) p.stamps = e->d_stamps;
         e->stamp_sum.assign(kStamps, 0.0);
-        (void)hipMalloc(&e->d_fstamps, (size_t)e->V * e->A * kStamps * 8);
+        (void)hipMalloc(&e->d_fstamps, (size_t)e->V * e->A * ((H + 7) / 8) * kStamps * 8);
         e->fstamp_sum.assign(kStamps, 0.0);
     }
 #endif
@@ -667,6 +672,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     std::memset(&f, 0, sizeof(f));
     f.model = c.model; f.V = e->V; f.H = H; f.A = e->A; f.nq = e->nq; f.qoff = e->qoff;
     f.state_f64 = c.state_f64; f.P = P;
+    f.tsz = e->fin_tsz; f.ts = e->fin_ts = (H + e->fin_tsz - 1) / e->fin_tsz;
     f.window = c.savgol_window; f.half = c.savgol_window / 2;
     for (int j = 0; j < c.savgol_window; ++j) f.sg[j] = e->sg_taps[c.savgol_window - 1 - j];
     f.coef = p.coef; f.dt = p.dt; f.dt2 = p.dt2; f.dt_d = c.dt;
@@ -689,9 +695,11 @@ void mppi_destroy(mppi_engine* e) {
         fprintf(stderr, "[mppi stamps] avg cycles per wave over %lld waves:", (long long)e->stamp_n);
         for (int i = 1; i <= 7; ++i) fprintf(stderr, " %s=%.0f", names[i], e->stamp_sum[i] / e->stamp_n);
         fprintf(stderr, "\n");
-        static const char* fn[] = {"", "loads", "accum", "eta-reduce", "col-reduce", "final-col", "outputs"};
+        static const char* fn[] = {"", "min", "accum", "eta-reduce", "col-reduce", "final-col", "outputs",
+                                   "param-copy", "rec-loads"};
         fprintf(stderr, "[mppi stamps] finalize avg cycles per block over %lld blocks:", (long long)e->fstamp_n);
-        for (int i = 1; i <= 6; ++i) fprintf(stderr, " %s=%.0f", fn[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
+        for (int i : {7, 8, 1, 2, 3, 4, 5, 6})
+            fprintf(stderr, " %s=%.0f", fn[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
         fprintf(stderr, "\n");
         (void)hipFree(e->d_stamps);
         (void)hipFree(e->d_fstamps);
@@ -702,7 +710,7 @@ void mppi_destroy(mppi_engine* e) {
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
-                   e->d_S, e->d_part, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w};
+                   e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -774,6 +782,14 @@ mppi_status mppi_bind_exchange(mppi_engine* e, float* d) {
     return MPPI_OK;
 }
 
+// the rollout's per-block partial records (DevParams::hdr / rdata layout)
+static void block_records(const mppi_engine* e, FinParams& f) {
+    const int64_t nb = e->dp.nb, H = e->H;
+    f.nrec = (int32_t)nb;
+    f.hdr = e->d_hdr; f.hdr_vs = nb * 4; f.hdr_rs = 4;
+    f.dat = e->d_rdata; f.d_vs = (int64_t)e->A * nb * H; f.d_as = nb * H; f.d_rs = H;
+}
+
 mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_rollout before mppi_set_state");
@@ -802,8 +818,7 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         FinParams f = e->fp;
         f.vc0 = e->h_vc[0];
         f.mode = 1;
-        f.rec = e->d_part; f.nrec = e->dp.nb;
-        f.rec_vstride = (int64_t)e->dp.nb * e->dp.P; f.rec_rstride = e->dp.P;
+        block_records(e, f);
         f.dst = e->d_exchange + slot * e->cfg.shard_rank;
         rc = mppi_launch_finalize(&f, e->stream);
         if (rc != 0) return fail(MPPI_ERR_HIP, "pack launch failed (%d)", rc);
@@ -817,12 +832,13 @@ mppi_status mppi_finalize(mppi_engine* e) {
     FinParams f = e->fp;
     f.vc0 = e->h_vc[0];
     f.mode = 0;
-    if (e->cfg.shard_count > 1) {
-        f.rec = e->d_exchange; f.nrec = e->cfg.shard_count;
-        f.rec_vstride = e->dp.P; f.rec_rstride = (int64_t)e->V * e->dp.P;
+    if (e->cfg.shard_count > 1) {   // slots [shard][v][P]: header then N[a][t]
+        const int64_t P = e->dp.P;
+        f.nrec = e->cfg.shard_count;
+        f.hdr = e->d_exchange; f.hdr_vs = P; f.hdr_rs = (int64_t)e->V * P;
+        f.dat = e->d_exchange + kHdr; f.d_vs = P; f.d_as = e->H; f.d_rs = (int64_t)e->V * P;
     } else {
-        f.rec = e->d_part; f.nrec = e->dp.nb;
-        f.rec_vstride = (int64_t)e->dp.nb * e->dp.P; f.rec_rstride = e->dp.P;
+        block_records(e, f);
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
@@ -851,11 +867,16 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
         // clock: wave 0 shader cycles vs 100 MHz realtime across the wave lifetime is not
         // stamped at the end; report cycles only
         e->stamp_n += (int64_t)nwaves;
-        const size_t nfb = (size_t)e->V * e->A;
+        const size_t nfb = (size_t)e->V * e->A * e->fin_ts;
         std::vector<unsigned long long> fs(nfb * kStamps);
         HIP_TRY(hipMemcpy(fs.data(), e->d_fstamps, fs.size() * 8, hipMemcpyDeviceToHost));
-        for (size_t b = 0; b < nfb; ++b)
-            for (int i = 1; i <= 6; ++i) e->fstamp_sum[i] += (double)(fs[b * kStamps + i] - fs[b * kStamps + i - 1]);
+        for (size_t b = 0; b < nfb; ++b) {
+            const unsigned long long* x = &fs[b * kStamps];
+            e->fstamp_sum[7] += (double)(x[7] - x[0]);   // kernarg copy + barrier
+            e->fstamp_sum[8] += (double)(x[8] - x[7]);   // record loads landed
+            e->fstamp_sum[1] += (double)(x[1] - x[8]);
+            for (int i = 2; i <= 6; ++i) e->fstamp_sum[i] += (double)(x[i] - x[i - 1]);
+        }
         e->fstamp_n += (int64_t)nfb;
     }
     const double* o = (const double*)e->h_out;
@@ -920,6 +941,52 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
         if ((st = mppi_finalize(e)) != MPPI_OK) return st;
     }
     return MPPI_OK;
+}
+
+mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
+    if (!e || n <= 0 || !rollout_us || !finalize_us) return fail(MPPI_ERR_INVALID_ARG, "mppi_kernel_timing: bad arguments");
+    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_kernel_timing is single-shard");
+    if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_kernel_timing needs device noise");
+    if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_kernel_timing before mppi_set_state");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t ub = sizeof(float) * e->V * e->H * e->A;
+    float* saved = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    mppi_status st = MPPI_OK;
+    DevParams p = e->dp;
+    p.vc0 = e->h_vc[0];
+    p.step_ctr = e->step_ctr;
+    FinParams f = e->fp;
+    f.vc0 = e->h_vc[0];
+    f.mode = 0;
+    block_records(e, f);
+    float ms0 = 0.0f, ms1 = 0.0f;
+    int rc = 0;
+#define KT_TRY(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) { st = fail(MPPI_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e)); goto done; } \
+    } while (0)
+    KT_TRY(hipMalloc(&saved, ub));
+    for (auto& x : ev) KT_TRY(hipEventCreate(&x));
+    KT_TRY(hipMemcpyAsync(saved, e->d_u_prev, ub, hipMemcpyDeviceToDevice, e->stream));
+    KT_TRY(hipEventRecord(ev[0], e->stream));
+    for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_rollout(&p, e->threads, e->stream);
+    KT_TRY(hipEventRecord(ev[1], e->stream));
+    for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_finalize(&f, e->stream);
+    KT_TRY(hipEventRecord(ev[2], e->stream));
+    KT_TRY(hipMemcpyAsync(e->d_u_prev, saved, ub, hipMemcpyDeviceToDevice, e->stream));
+    KT_TRY(hipStreamSynchronize(e->stream));
+    if (rc != 0) { st = fail(MPPI_ERR_HIP, "kernel launch failed (%d)", rc); goto done; }
+    KT_TRY(hipEventElapsedTime(&ms0, ev[0], ev[1]));
+    KT_TRY(hipEventElapsedTime(&ms1, ev[1], ev[2]));
+    *rollout_us = 1e3 * ms0 / n;
+    *finalize_us = 1e3 * ms1 / n;
+#undef KT_TRY
+done:
+    for (auto x : ev) if (x) (void)hipEventDestroy(x);
+    if (saved) (void)hipFree(saved);
+    return st;
 }
 
 mppi_status mppi_synchronize(mppi_engine* e) {

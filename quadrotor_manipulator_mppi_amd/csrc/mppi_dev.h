@@ -75,7 +75,8 @@ struct DevParams {
     float* traj;             // (V,C,K,H) SoA planes
     float* noise_out;        // (V,K,H,A)
     float* S;                // (V,K)
-    float* part;             // (V,nb,P)
+    float* hdr;              // (V,nb,4) partial record headers: rho, eta, eta2, nan
+    float* rdata;            // (V,A,nb,H) partial record bodies, dim-major
     unsigned long long* stamps;   // diagnostic s_memtime stamps per wave (MPPI_STAMPS), else null
 };
 constexpr int kStamps = 10;
@@ -84,7 +85,11 @@ constexpr int kStamps = 10;
 struct FinParams {
     int32_t model, V, H, A, nq, qoff, state_f64;
     int32_t nrec;            // records to combine per vehicle
-    int64_t rec_vstride, rec_rstride;   // floats
+    int32_t ts, tsz;         // t-slices per action dim (grid.x = A*ts), slice length
+    const float* hdr;        // record headers (rho, eta, eta2, nan) at hdr + v*hdr_vs + r*hdr_rs
+    int64_t hdr_vs, hdr_rs;
+    const float* dat;        // record bodies N[a][t] at dat + v*d_vs + a*d_as + r*d_rs + t
+    int64_t d_vs, d_as, d_rs;
     int32_t P;
     int32_t mode;            // 0 = final, 1 = pack into dst slot
     int32_t window, half;
@@ -92,7 +97,6 @@ struct FinParams {
     double dt_d;
     float sg[kMaxW];         // SavGol taps (already flipped for the correlation)
     VehicleConst vc0;        // V == 1
-    const float* rec;        // records base
     float* dst;              // pack destination (slot base, vehicle stride P)
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;

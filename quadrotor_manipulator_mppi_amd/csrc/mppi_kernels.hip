@@ -19,6 +19,7 @@
 // wave writes 64 consecutive floats (256 B).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "mppi_dev.h"
@@ -314,27 +315,37 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
     return r;
 }
 
-template <int MODEL, int NA, int NCH, int LSEG, bool F64>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
 __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     constexpr int R = 64 / LSEG;
     constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    // The whole parameter block (scalars, Sigma diagonal, vehicle-0 constants,
-    // joint table) is copied into LDS by all threads in ONE round trip: kernel
-    // arguments are fresh memory every launch, and scattered scalar loads of
-    // them (rematerialised under SGPR pressure) cost a memory round trip each.
-    __shared__ DevParams ps;
+    // Scalars and (V == 1) the vehicle constants are read from the kernel
+    // arguments with scalar loads (SGPR operands, no LDS latency in the hot
+    // phases); the joint table and (V > 1) the vehicle block go to LDS.
+    __shared__ JointDev jnt[kMaxJ];
     __shared__ VehicleConst vcv;
+    const DevParams& p = pk;
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
     STAMP(0);
+    // warm every kernel-argument cache line the hot phases touch, in one batch
     {
-        const int* src = (const int*)&pk;
-        int* dst = (int*)&ps;
-        for (int i = tid; i < (int)(sizeof(DevParams) / 4); i += blockDim.x) dst[i] = src[i];
-        if (pk.V > 1) {
+        const float* kp = (const float*)&pk;
+        float w0 = 0.0f;
+#pragma unroll
+        for (int o = 0; o < (int)((offsetof(DevParams, joints)) / 4); o += 16) w0 += kp[o];
+        asm volatile("" :: "s"(w0));
+    }
+    {
+        if (MODEL != MPPI_MODEL_DRONE) {
+            const int jw = pk.nj * (int)(sizeof(JointDev) / 4);
+            const int* js = (const int*)pk.joints;
+            for (int i = tid; i < jw; i += blockDim.x) ((int*)jnt)[i] = js[i];
+        }
+        if (!VONE) {
             const int* vs = (const int*)(pk.vc + v);
             for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
         }
@@ -352,10 +363,8 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
                              pk.seed_hi);
     }
     lds_barrier();
-    const DevParams& p = ps;
-    const VehicleConst& vc = (pk.V == 1) ? ps.vc0 : vcv;
-    const JointDev* jnt = ps.joints;
-    const float* sdiag = ps.sdiag;
+    const VehicleConst& vc = VONE ? pk.vc0 : vcv;
+    const float* sdiag = pk.sdiag;
     const int H = pk.H, K = pk.K;
     STAMP(1);
 
@@ -367,15 +376,14 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     float rho_w = INFINITY, eta_w = 0.0f, eta2_w = 0.0f;   // wave-uniform
     bool nan_w = false;
 
-    for (int it = 0; it < p.iters; ++it) {
-        // Launder the loop-invariant scalars through empty asm: keeps the compiler
-        // from hoisting the Philox key schedule, the 19 trajectory-plane offsets and
-        // the LDS constants out of the group loop (SGPR pressure -> spills).
-        asm volatile("" ::: "memory");
-        uint32_t seed_lo = pk.seed_lo, seed_hi = pk.seed_hi;
-        int plane_i = K * H;
+    // One group of R rollouts per wave.  Written as a lambda so the common
+    // single-group launch (iters == 1, e.g. K=4096 H=32) is straight-line code:
+    // no loop-invariant hoisting of address math / key schedules into SGPRs.
+    auto group = [&](const int it) {
+        asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
+        const uint32_t seed_lo = pk.seed_lo, seed_hi = pk.seed_hi;
+        const int plane_i = K * H;
         float* traj_base = pk.traj;
-        asm volatile("" : "+s"(seed_lo), "+s"(seed_hi), "+s"(plane_i), "+s"(traj_base));
         const int g = blockIdx.x + it * p.nb;
         const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
@@ -604,15 +612,21 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
                 for (int a = 0; a < NA; ++a) acc[c][a] = acc[c][a] * f + e_mine * eps[c][a];
             rho_w = rn;
         }
+    };
+    if (p.iters == 1) {
+        group(0);
+    } else {
+        for (int it = 0; it < p.iters; ++it) group(it);
     }
     STAMP(5);
 
     // ---- cross-wave combine in LDS -> one partial record per block
     //      LDS: [nw][4 + NCH*64*NA]; every lane (all R segments) deposits acc
-    float* wsh = smem + ((HA + 3) & ~3);
+    float* wsh = smem + ((HA + 3) & ~3);           // always 8 wave slots (unrolled reads)
     const int wstride = 4 + NCH * 64 * NA;
     float* mine = wsh + wid * wstride;
     if (lane == 0) { mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f; }
+    for (int i = nw * wstride + tid; i < 8 * wstride; i += blockDim.x) wsh[i] = 0.0f;   // absent waves
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -622,12 +636,12 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     __shared__ float fw[16];
     float rho_b = INFINITY;
     for (int w = 0; w < nw; ++w) rho_b = fminf(rho_b, wsh[w * wstride]);
-    if (tid < nw) {
-        const float rw = wsh[tid * wstride];
+    if (tid < 8) {
+        const float rw = (tid < nw) ? wsh[tid * wstride] : INFINITY;
         fw[tid] = (rw == INFINITY) ? 0.0f : __expf(p.coef * (rw - rho_b));
     }
     lds_barrier();
-    float* rec = p.part + ((size_t)v * p.nb + blockIdx.x) * p.P;
+    float* hb = p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4;
     if (tid == 0) {
         float eta = 0.0f, eta2 = 0.0f, nanf = 0.0f;
         for (int w = 0; w < nw; ++w) {
@@ -635,39 +649,39 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
             eta2 += fw[w] * fw[w] * wsh[w * wstride + 2];
             nanf = fmaxf(nanf, wsh[w * wstride + 3]);
         }
-        rec[0] = rho_b; rec[1] = eta; rec[2] = eta2; rec[3] = nanf;
+        *reinterpret_cast<float4*>(hb) = make_float4(rho_b, eta, eta2, nanf);
     }
-    // record body a-major: N[a*H + t] = sum_w f_w sum_segments acc_w[seg*L + t]
+    // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t]
     for (int i = tid; i < HA; i += blockDim.x) {
         const int a = i / H, t = i - a * H;
         const int c = t >> 6, tl = t & 63;
+        float sw[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {   // slots of absent waves hold 0 (zeroed) and fw = 0
+            sw[w] = 0.0f;
+#pragma unroll
+            for (int sg = 0; sg < R; ++sg) sw[w] += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
+        }
         float s = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            if (w < nw) {
-                float sw = 0.0f;
-#pragma unroll
-                for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
-                s += fw[w] * sw;
-            }
-        }
-        rec[kHdr + i] = s;
+        for (int w = 0; w < 8; ++w) s += fw[w] * sw[w];
+        p.rdata[(((size_t)v * NA + a) * p.nb + blockIdx.x) * H + t] = s;
     }
     STAMP(7);
 }
 
 // =============================================================================
-// k_finalize: grid (A, V); block a owns action dim a of vehicle v.
+// k_finalize: grid (A*ts, V); block (a, slice) owns t in one slice of action
+// dim a of vehicle v (plus the SavGol halo it reads).
 //   1. rho = min_r rho_r                     (record headers)
 //   2. f_r = exp(-(rho_r - rho)/lambda); eta = sum f_r eta_r   (fp64 sums)
-//   3. N[t] = sum_r f_r N_r[a][t]            (16-byte loads, all in flight)
+//   3. N[t] = sum_r f_r N_r[a][t]            (all loads in flight, one pass)
 //   PACK: write (rho, eta, eta2, nan | N) into the shard's exchange slot.
 //   FINAL: w_eps = N/eta, SavGol (symmetric pad), u += w_eps, outputs written
 //          straight into mapped pinned host memory (no D2H copy).
 // =============================================================================
 constexpr int kFinThreads = 256;
 constexpr int kMaxRec = 4096;
-constexpr int kNPT = 8;
 
 // DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
 // result lands in lane 63 and is broadcast with readlane (no LDS round trips).
@@ -707,8 +721,8 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 #define FSTAMP(i)                                                                    \
     do {                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                           \
-        if (p.stamps && threadIdx.x == 0)                                            \
-            p.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps + (i)] = \
+        if (pk.stamps && threadIdx.x == 0)                                           \
+            pk.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps + (i)] = \
                 __builtin_amdgcn_s_memtime();                                        \
         __builtin_amdgcn_sched_barrier(0);                                           \
     } while (0)
@@ -717,35 +731,36 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 #endif
 
 __global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
+    // grid (A * ts, V): block (a, slice) owns t in [t_lo, t_hi) of action dim a
+    // and reads the records' columns for that slice plus the SavGol halo -- the
+    // record reads are spread over A*ts CUs (a single CU streams ~10 B/clk).
     constexpr int NWV = kFinThreads / 64;
-    __shared__ FinParams ps;   // one-round-trip copy of the kernel arguments (see k_rollout)
-    {
-        const int* src = (const int*)&pk;
-        for (int i = threadIdx.x; i < (int)(sizeof(FinParams) / 4); i += kFinThreads) ((int*)&ps)[i] = src[i];
-    }
-    lds_barrier();
-    const FinParams& p = ps;
-    __shared__ float4 part4[kFinThreads];
-    __shared__ float wcol[MPPI_MAX_HORIZON + 2 * kMaxW];
+    constexpr int kNPT = 16;                 // records per thread in the one-pass path
+    constexpr int kWin = 16 + 2 * 15;        // max slice + halo
+    __shared__ float nsum[kFinThreads];
+    __shared__ float wcol[kWin];
     __shared__ float shm[2 * NWV];
     __shared__ double shd[2 * NWV];
-    const int a = blockIdx.x, v = blockIdx.y, tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
+    const FinParams& p = pk;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int a = blockIdx.x / p.ts, sl = blockIdx.x - a * p.ts, v = blockIdx.y;
     FSTAMP(0);
-    const int H = p.H, n = p.nrec;
-    const float* recs = p.rec + (size_t)v * p.rec_vstride;
-    const size_t rs = (size_t)p.rec_rstride;
+    const int H = p.H, n = p.nrec, hf = p.half;
+    const int t_lo = sl * p.tsz, t_hi = min(H, t_lo + p.tsz);
+    const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1)
+    const float* hdr = p.hdr + (size_t)v * p.hdr_vs;
+    const size_t hrs = (size_t)p.hdr_rs;
+    const float* col = p.dat + (size_t)v * p.d_vs + (size_t)a * p.d_as + w0;
+    const size_t drs = (size_t)p.d_rs;
+    float* up = p.u_prev + (size_t)v * H * p.A;
+    const float uold0 = (tid == 0 && sl == 0) ? up[a] : 0.0f;   // the old u_prev[0] (mppi.py:157)
+    FSTAMP(7);
 
-    // Thread (g, q): column chunk q (4 consecutive t when H % 4 == 0, else 1 t)
-    // of records g, g + rows, ...  Headers and column data are loaded in one
-    // pass (kNPT records per thread, all loads in flight) when n <= rows*kNPT.
-    const bool vec = (H & 3) == 0;
-    const int tpr = vec ? (H >> 2) : H;
-    const int rows = kFinThreads / tpr;
-    const int g = tid / tpr, q = tid - g * tpr;
+    // thread (g, q): window column q of records g, g + rows, ...
+    const int rows = kFinThreads / W;
+    const int g = tid / W, q = tid - g * W;
     const bool active = g < rows;
-    const float* col = recs + kHdr + (size_t)a * H;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float acc = 0.0f;
     double eta = 0.0, eta2 = 0.0;
     float rho, nanflag;
     auto block_minmax = [&](float m, float nf) {
@@ -757,62 +772,56 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
 #pragma unroll
         for (int i = 1; i < NWV; ++i) { rho = fminf(rho, shm[i]); nanflag = fmaxf(nanflag, shm[NWV + i]); }
     };
-    if (p.dbg & 1) {          // diagnostic: skip the record loads
-        rho = 0.0f; nanflag = 0.0f;
-    } else if (n <= rows * kNPT) {
-        float4 hd[kNPT], xv[kNPT];
+    if (n <= rows * kNPT) {   // one pass: every load in flight before the reductions
+        float4 hd[kNPT];
+        float xv[kNPT];
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
             const int r = g + i * rows;
             const bool ok = active && r < n;
-            const size_t ro = (size_t)(ok ? r : 0) * rs;
-            hd[i] = *reinterpret_cast<const float4*>(recs + ro);
-            if (vec) xv[i] = *reinterpret_cast<const float4*>(col + ro + 4 * q);
-            else xv[i] = make_float4(col[ro + q], 0.f, 0.f, 0.f);
-            if (!ok) { hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f); xv[i] = make_float4(0.f, 0.f, 0.f, 0.f); }
+            const size_t rr = (size_t)(ok ? r : 0);
+            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * hrs);
+            xv[i] = col[rr * drs + q];
+            if (!ok) { hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f); xv[i] = 0.0f; }
         }
+        FSTAMP(8);
         float m = INFINITY, nf = 0.0f;
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nf = fmaxf(nf, hd[i].w); }
-        FSTAMP(1);
         block_minmax(m, nf);
+        FSTAMP(1);
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
             const float f = (hd[i].x == INFINITY) ? 0.0f : __expf(p.coef * (hd[i].x - rho));
-            acc.x = fmaf(f, xv[i].x, acc.x); acc.y = fmaf(f, xv[i].y, acc.y);
-            acc.z = fmaf(f, xv[i].z, acc.z); acc.w = fmaf(f, xv[i].w, acc.w);
+            acc = fmaf(f, xv[i], acc);
             if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
         }
-    } else {
+    } else {                  // two passes (many records)
         float m = INFINITY, nf = 0.0f;
         for (int r = tid; r < n; r += kFinThreads) {
-            m = fminf(m, recs[r * rs]);
-            nf = fmaxf(nf, recs[r * rs + 3]);
+            const float4 h4 = *reinterpret_cast<const float4*>(hdr + (size_t)r * hrs);
+            m = fminf(m, h4.x);
+            nf = fmaxf(nf, h4.w);
         }
-        FSTAMP(1);
+        FSTAMP(8);
         block_minmax(m, nf);
+        FSTAMP(1);
         if (active) {
-#pragma unroll 4
+#pragma unroll 8
             for (int r = g; r < n; r += rows) {
-                const float4 hd = *reinterpret_cast<const float4*>(recs + r * rs);
-                const float f = (hd.x == INFINITY) ? 0.0f : __expf(p.coef * (hd.x - rho));
-                float4 x;
-                if (vec) x = *reinterpret_cast<const float4*>(col + r * rs + 4 * q);
-                else x = make_float4(col[r * rs + q], 0.f, 0.f, 0.f);
-                acc.x = fmaf(f, x.x, acc.x); acc.y = fmaf(f, x.y, acc.y);
-                acc.z = fmaf(f, x.z, acc.z); acc.w = fmaf(f, x.w, acc.w);
-                if (q == 0) { eta += (double)f * hd.y; eta2 += (double)f * f * hd.z; }
+                const float4 h4 = *reinterpret_cast<const float4*>(hdr + (size_t)r * hrs);
+                const float f = (h4.x == INFINITY) ? 0.0f : __expf(p.coef * (h4.x - rho));
+                acc = fmaf(f, col[(size_t)r * drs + q], acc);
+                if (q == 0) { eta += (double)f * h4.y; eta2 += (double)f * f * h4.z; }
             }
         }
     }
     FSTAMP(2);
-    // eta / eta2: DPP wave sums, then the NWV wave totals
     {
         const double e1 = wave_sum_f64(eta), e2 = wave_sum_f64(eta2);
         if (lane == 0) { shd[wv] = e1; shd[NWV + wv] = e2; }
     }
-    // column partials: log-step tree over g in LDS (no serial dependent chains)
-    part4[tid] = acc;
+    nsum[tid] = active ? acc : 0.0f;
     lds_barrier();
     eta = shd[0]; eta2 = shd[NWV];
 #pragma unroll
@@ -820,63 +829,50 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
     FSTAMP(3);
     int span = 1;
     while (span < rows) span <<= 1;
-    for (int s = span >> 1; s > 0; s >>= 1) {
-        if (active && g < s && g + s < rows) {
-            const float4 o = part4[(g + s) * tpr + q];
-            float4 x = part4[tid];
-            x.x += o.x; x.y += o.y; x.z += o.z; x.w += o.w;
-            part4[tid] = x;
-        }
+    for (int s = span >> 1; s > 0; s >>= 1) {   // log-step tree over g
+        if (active && g < s && g + s < rows) nsum[tid] += nsum[tid + s * W];
         lds_barrier();
     }
-    for (int t = tid; t < H; t += kFinThreads) {
-        const float4 x = part4[vec ? (t >> 2) : t];
-        const int l4 = vec ? (t & 3) : 0;
-        wcol[kMaxW + t] = l4 == 0 ? x.x : l4 == 1 ? x.y : l4 == 2 ? x.z : x.w;
-    }
+    if (tid < W) wcol[tid] = nsum[tid];
     lds_barrier();
     FSTAMP(4);
 
-    if (p.mode == 1) {   // PACK into this shard's exchange slot
+    if (p.mode == 1) {   // PACK raw sums into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
-        if (a == 0 && tid == 0) {
+        if (a == 0 && sl == 0 && tid == 0) {
             dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanflag;
         }
-        for (int t = tid; t < H; t += kFinThreads) dst[kHdr + a * H + t] = wcol[kMaxW + t];
+        for (int t = t_lo + tid; t < t_hi; t += kFinThreads) dst[kHdr + a * H + t] = wcol[t - w0];
         return;
     }
-    if (p.dbg & 2) return;    // diagnostic: stop after the reduction
 
-    // FINAL: w_eps = N/eta, SavGol (symmetric pad, svg_filter.py:58), u += w_eps
+    // FINAL: w_eps = N/eta over the window, SavGol with the reference's symmetric
+    // pad (svg_filter.py:58: index -i-1 left of 0, 2H-1-i right of H-1), u += w_eps
     const float etaf = (nanflag > 0.0f) ? NAN : (float)eta;
-    float* up = p.u_prev + (size_t)v * H * p.A;
-    const float uold0 = up[a];
-    const int hf = p.half;
-    float wv_t = 0.0f;
-    if (tid < H) {
-        wv_t = wcol[kMaxW + tid] / etaf;
-        wcol[kMaxW + tid] = wv_t;
-        if (p.wraw) p.wraw[((size_t)v * H + tid) * p.A + a] = wv_t;
+    if (tid < W) {
+        const float w = wcol[tid] / etaf;
+        wcol[tid] = w;
+        const int t = w0 + tid;
+        if (p.wraw && t >= t_lo && t < t_hi) p.wraw[((size_t)v * H + t) * p.A + a] = w;
     }
     lds_barrier();
-    if (tid < hf) {   // [d_{h-1} .. d_0 | d | d_{N-1} .. d_{N-h}]
-        wcol[kMaxW - 1 - tid] = wcol[kMaxW + tid];
-        wcol[kMaxW + H + tid] = wcol[kMaxW + H - 1 - tid];
-    }
-    lds_barrier();
-    for (int t = tid; t < H; t += kFinThreads) {
-        float s = 0.0f;
-        for (int j = 0; j < p.window; ++j) s += p.sg[j] * wcol[kMaxW - hf + t + j];
-        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * p.A + a] = s;
-        const float un = up[t * p.A + a] + s;
+    float u0new = 0.0f;
+    for (int t = t_lo + tid; t < t_hi; t += kFinThreads) {
+        float sm = 0.0f;
+        for (int j = 0; j < p.window; ++j) {
+            int idx = t + j - hf;
+            idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
+            sm += p.sg[j] * wcol[idx - w0];
+        }
+        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * p.A + a] = sm;
+        const float un = up[t * p.A + a] + sm;
         up[t * p.A + a] = un;
-        if (t == 0) wcol[0] = un;   // u0 for the output thread
+        if (t == 0) u0new = un;
     }
-    lds_barrier();
     FSTAMP(5);
-    if (tid == 0 && !(p.dbg & 4)) {
+    if (sl == 0 && tid == 0) {
 #pragma clang fp contract(off)
-        const float u0 = wcol[0];
+        const float u0 = u0new;
         p.u0[(size_t)v * p.A + a] = u0;
         const VehicleConst& vc = (p.V == 1) ? p.vc0 : p.vc[v];
         double* out = p.out + (size_t)v * p.out_dim;
@@ -946,9 +942,11 @@ __global__ void k_philox(uint64_t seed, uint32_t step, int veh, int64_t k0, int 
 // =============================================================================
 template <int MODEL, int NA, int NCH, int LSEG, bool F64>
 static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
-    const int nw = threads / 64;
-    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + nw * (4 + NCH * 64 * NA)) * sizeof(float);
-    hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
+    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
+    if (p.V == 1)
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
+    else
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
     return (int)hipGetLastError();
 }
 
@@ -970,20 +968,17 @@ extern "C" int mppi_launch_rollout(const DevParams* p, int threads, void* stream
         case MPPI_MODEL_ARM:
             if (p->A == 7) return p->state_f64 ? dispatch_geom<MPPI_MODEL_ARM, 7, true>(*p, threads, s)
                                                : dispatch_geom<MPPI_MODEL_ARM, 7, false>(*p, threads, s);
-            if (p->A == 6) return p->state_f64 ? dispatch_geom<MPPI_MODEL_ARM, 6, true>(*p, threads, s)
-                                               : dispatch_geom<MPPI_MODEL_ARM, 6, false>(*p, threads, s);
             break;
         case MPPI_MODEL_WHOLEBODY:
             if (p->A == 10) return dispatch_geom<MPPI_MODEL_WHOLEBODY, 10, false>(*p, threads, s);
-            if (p->A == 9) return dispatch_geom<MPPI_MODEL_WHOLEBODY, 9, false>(*p, threads, s);
             break;
     }
     return -1;
 }
 
 extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
-    if (p->nrec > kMaxRec || p->H > MPPI_MAX_HORIZON) return -1;
-    hipLaunchKernelGGL(k_finalize, dim3(p->A, p->V), dim3(kFinThreads), 0, (hipStream_t)stream, *p);
+    if (p->nrec > kMaxRec || p->H > MPPI_MAX_HORIZON || p->tsz + 2 * p->half > 16 + 2 * 15) return -1;
+    hipLaunchKernelGGL(k_finalize, dim3(p->A * p->ts, p->V), dim3(kFinThreads), 0, (hipStream_t)stream, *p);
     return (int)hipGetLastError();
 }
 

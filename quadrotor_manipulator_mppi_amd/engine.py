@@ -230,6 +230,12 @@ class Engine:
         return {"rollout_ms_total": r.value, "finalize_ms_total": f.value,
                 "n_rollout": rn.value, "n_finalize": fn.value}
 
+    def kernel_timing(self, n: int = 200):
+        """(rollout_us, finalize_us): average device time per launch, launched back to back."""
+        r, f = C.c_double(), C.c_double()
+        capi.check(self._L.mppi_kernel_timing(self._h, n, C.byref(r), C.byref(f)), "kernel_timing")
+        return r.value, f.value
+
     def rollout_bytes(self) -> int:
         return int(self._L.mppi_rollout_bytes(C.byref(self.cfg)))
 
