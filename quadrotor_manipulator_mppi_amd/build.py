@@ -19,9 +19,13 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libmppi_hip.so")
 LIB_STAMPS = os.path.join(LIB_DIR, "libmppi_hip_stamps.so")   # diagnostic phase-stamp build
-SOURCES = ["mppi_kernels.hip", "mppi_capi.cpp"]
-HEADERS = ["mppi_dev.h", os.path.join("..", "..", "include", "mppi_hip.h")]
+# (source, extra flags).  The rollout is built without the SLP vectorizer: its
+# v_pk_* pairings cost more register moves than they save and raise the kernel
+# from 110 to 184 VGPRs (2 instead of 4 waves per SIMD) -- DESIGN.md §kernels.
+SOURCES = [("mppi_rollout.hip", ["-fno-slp-vectorize"]), ("mppi_finalize.hip", []), ("mppi_capi.cpp", [])]
+HEADERS = ["mppi_dev.h", "mppi_device.h", os.path.join("..", "..", "include", "mppi_hip.h")]
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
+EXTRA = os.environ.get("MPPI_HIPCC_EXTRA", "").split()   # experiment flags (tools/), empty in production
 
 
 def hipcc() -> str:
@@ -35,27 +39,40 @@ def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    deps = [os.path.join(CSRC, s) for s, _ in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
 def build(force: bool = False, debug: bool = False, verbose: bool = False, stamps: bool = False) -> str:
-    out = LIB_STAMPS if stamps else LIB
+    out = os.environ.get("MPPI_BUILD_OUT") or (LIB_STAMPS if stamps else LIB)
     if not force and not stamps and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = out + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-           "-O1" if debug else "-O3", "-I", os.path.join(ROOT, "include"),
-           "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-o", tmp] + (["-DMPPI_STAMPS"] if stamps else []) + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd))
+    base = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O1" if debug else "-O3",
+            "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-Wno-unused-variable"] + \
+        (["-DMPPI_STAMPS"] if stamps else []) + EXTRA
+    objdir = os.path.join(LIB_DIR, "obj" + ("_stamps" if stamps else ""))
+    os.makedirs(objdir, exist_ok=True)
+    objs, procs = [], []
+    for src, flags in SOURCES:   # compile the translation units in parallel
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = base + flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+        objs.append(obj)
+    for src, pr in procs:
+        so, se = pr.communicate()
+        if pr.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src} ({pr.returncode}):\n{so}\n{se}")
+        if verbose and se.strip():
+            print(se)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
-    if verbose and res.stderr.strip():
-        print(res.stderr)
+        raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, out)
     return out
 

@@ -245,6 +245,16 @@ void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xy
 }  // namespace
 
 // =============================================================================
+// MPPI_STAMPS diagnostics: stamp indices in program order and the phase each
+// difference measures (see the STAMP calls in mppi_rollout.hip / mppi_finalize.hip).
+static const std::vector<int> kRollStampOrder = {0, 8, 9, 10, 1, 2, 3, 4, 5, 11, 6, 12, 7};
+static const char* const kRollStampNames[] = {"", "kernarg", "loads(waited)", "philox0", "barrier", "noise",
+                                              "integrator", "fk+cost", "S+softmin", "deposit", "combine-barrier",
+                                              "fw", "record"};
+static const std::vector<int> kFinStampOrder = {0, 7, 8, 1, 2, 3, 4, 5, 6};
+static const char* const kFinStampNames[] = {"", "setup", "rec-loads", "min", "accum", "eta-reduce",
+                                             "col-reduce", "final-col", "outputs"};
+
 struct mppi_engine {
     mppi_config cfg;
     int K, H, A, V, nq, qoff, state_dim, out_dim, C, threads;
@@ -690,16 +700,12 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
 void mppi_destroy(mppi_engine* e) {
     if (!e) return;
     if (e->d_stamps && e->stamp_n) {
-        static const char* names[] = {"", "lds-init", "noise", "integrator", "fk+cost", "S+softmin(rest)",
-                                      "combine-barrier", "record"};
-        fprintf(stderr, "[mppi stamps] avg cycles per wave over %lld waves:", (long long)e->stamp_n);
-        for (int i = 1; i <= 7; ++i) fprintf(stderr, " %s=%.0f", names[i], e->stamp_sum[i] / e->stamp_n);
-        fprintf(stderr, "\n");
-        static const char* fn[] = {"", "min", "accum", "eta-reduce", "col-reduce", "final-col", "outputs",
-                                   "param-copy", "rec-loads"};
-        fprintf(stderr, "[mppi stamps] finalize avg cycles per block over %lld blocks:", (long long)e->fstamp_n);
-        for (int i : {7, 8, 1, 2, 3, 4, 5, 6})
-            fprintf(stderr, " %s=%.0f", fn[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
+        fprintf(stderr, "[mppi stamps] rollout avg cycles per wave over %lld waves:", (long long)e->stamp_n);
+        for (size_t i = 1; i < kRollStampOrder.size(); ++i)
+            fprintf(stderr, " %s=%.0f", kRollStampNames[i], e->stamp_sum[i] / e->stamp_n);
+        fprintf(stderr, "\n[mppi stamps] finalize avg cycles per block over %lld blocks:", (long long)e->fstamp_n);
+        for (size_t i = 1; i < kFinStampOrder.size(); ++i)
+            fprintf(stderr, " %s=%.0f", kFinStampNames[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
         fprintf(stderr, "\n");
         (void)hipFree(e->d_stamps);
         (void)hipFree(e->d_fstamps);
@@ -862,20 +868,17 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
         HIP_TRY(hipMemcpy(st.data(), e->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
         for (size_t w = 0; w < nwaves; ++w) {
             const unsigned long long* x = &st[w * kStamps];
-            for (int i = 1; i <= 7; ++i) e->stamp_sum[i] += (double)(x[i] - x[i - 1]);
+            for (size_t i = 1; i < kRollStampOrder.size(); ++i)
+                e->stamp_sum[i] += (double)(x[kRollStampOrder[i]] - x[kRollStampOrder[i - 1]]);
         }
-        // clock: wave 0 shader cycles vs 100 MHz realtime across the wave lifetime is not
-        // stamped at the end; report cycles only
         e->stamp_n += (int64_t)nwaves;
         const size_t nfb = (size_t)e->V * e->A * e->fin_ts;
         std::vector<unsigned long long> fs(nfb * kStamps);
         HIP_TRY(hipMemcpy(fs.data(), e->d_fstamps, fs.size() * 8, hipMemcpyDeviceToHost));
         for (size_t b = 0; b < nfb; ++b) {
             const unsigned long long* x = &fs[b * kStamps];
-            e->fstamp_sum[7] += (double)(x[7] - x[0]);   // kernarg copy + barrier
-            e->fstamp_sum[8] += (double)(x[8] - x[7]);   // record loads landed
-            e->fstamp_sum[1] += (double)(x[1] - x[8]);
-            for (int i = 2; i <= 6; ++i) e->fstamp_sum[i] += (double)(x[i] - x[i - 1]);
+            for (size_t i = 1; i < kFinStampOrder.size(); ++i)
+                e->fstamp_sum[i] += (double)(x[kFinStampOrder[i]] - x[kFinStampOrder[i - 1]]);
         }
         e->fstamp_n += (int64_t)nfb;
     }

@@ -79,7 +79,7 @@ struct DevParams {
     float* rdata;            // (V,A,nb,H) partial record bodies, dim-major
     unsigned long long* stamps;   // diagnostic s_memtime stamps per wave (MPPI_STAMPS), else null
 };
-constexpr int kStamps = 10;
+constexpr int kStamps = 16;
 
 // Finalize / pack kernel parameters.
 struct FinParams {

@@ -1,0 +1,69 @@
+// mppi_device.h -- device helpers shared by the gfx950 kernels (rollout, finalize).
+// Internal: included only by mppi_rollout.hip / mppi_finalize.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mppi_dev.h"
+
+using namespace mppi;
+
+namespace {
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
+// (lgkmcnt) but NOT for its outstanding global stores (vmcnt), which
+// __syncthreads() would drain -- nothing in these kernels reads its own
+// trajectory / record stores back, so the store round trip stays off the
+// critical path.  The memory clobber keeps the compiler from moving LDS
+// accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ----------------------------------------------------------------- DPP helpers
+// dpp_ctrl encodings (GFX9): row_shr:n = 0x110+n, wave_shr:1 = 0x138,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double x) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWMASK, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f32(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWMASK, 0xF, false));
+}
+
+// Inclusive prefix sum inside segments of L lanes (L in {16, 32, 64}).
+__device__ __forceinline__ double seg_scan(double x, int L) {
+    x += dpp_f64<0x111, 0xF>(x);
+    x += dpp_f64<0x112, 0xF>(x);
+    x += dpp_f64<0x114, 0xF>(x);
+    x += dpp_f64<0x118, 0xF>(x);
+    if (L >= 32) x += dpp_f64<0x142, 0xA>(x);
+    if (L >= 64) x += dpp_f64<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ double read_lane_f64(double x, int lane) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// DPP helpers with bound_ctrl (out-of-row sources read 0): no zeroing moves.
+template <int CTRL>
+__device__ __forceinline__ double shr_f64(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(x), __double2loint(x), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(x), __double2hiint(x), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ float read_lane_f32(float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+}  // namespace
