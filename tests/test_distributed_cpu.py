@@ -1,0 +1,127 @@
+"""CPU tests of the multi-GPU exchange protocol over gloo.
+
+The device path is: every rank's rollout folds its samples into one partial
+record per vehicle, PACK writes it into slot ``rank`` of a zeroed (G, V, P)
+buffer, ONE ``all_reduce(SUM)`` hands every rank all G slots, and every rank's
+finalize combines them.  These tests run the same protocol with the oracle's
+fp64 shard partials standing in for the rollout (no GPU here): the slot layout,
+the zero-padded SUM-as-gather, and the rescale-by-exp(-(rho_g - rho)/lambda)
+combine are checked against the unsharded control step of the golden fixtures.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_golden
+from oracle import mppi_oracle as O
+from quadrotor_manipulator_mppi_amd.distributed import HDR, all_reduce_slots, combine_slots
+
+
+def _slot_len(A, H):
+    return (HDR + A * H + 3) & ~3   # P: header + N[a][t], rounded to 16 B (mppi_capi.cpp)
+
+
+def _pack(S, eps, lam, P):
+    """One shard's record in the engine's exchange layout: [rho, eta, eta2, nan | N a-major]."""
+    rho, eta, N = O.shard_partial(torch.as_tensor(S), torch.as_tensor(eps), lam)
+    f = torch.exp(-(torch.as_tensor(S).double() - rho) / lam)
+    rec = np.zeros(P, np.float32)
+    H, A = N.shape
+    rec[0], rec[1], rec[2], rec[3] = float(rho), float(eta), float((f * f).sum()), 0.0
+    rec[HDR:HDR + A * H] = N.numpy().T.reshape(-1)
+    return rec
+
+
+def _shards(K, G):
+    b = np.linspace(0, K, G + 1).astype(int)
+    return [(b[g], b[g + 1]) for g in range(G)]
+
+
+@pytest.mark.parametrize("name,G", [("arm_k100_h32_f64.npz", 2), ("arm_k100_h32_f64.npz", 5),
+                                    ("drone_k256_h32.npz", 4), ("wholebody_k32_h64.npz", 3)])
+def test_combine_slots_matches_unsharded(name, G):
+    d = load_golden(name)
+    S, eps, lam = d["s0_S"], d["s0_noise"], float(d["lam"])
+    K, H, A = eps.shape
+    P = _slot_len(A, H)
+    slots = np.stack([_pack(S[a:b], eps[a:b], lam, P) for a, b in _shards(K, G)])
+    got = combine_slots(slots, lam, H, A)
+    rho, eta, N = O.shard_partial(torch.as_tensor(S), torch.as_tensor(eps), lam)
+    want = (N / eta).numpy()
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=1e-6 * np.abs(want).max())
+    # and the reference's own fp32 weighted sum (mppi.py:143) within its rounding
+    np.testing.assert_allclose(got, d["s0_w_eps_raw"], rtol=1e-3, atol=2e-4 * np.abs(want).max())
+
+
+def test_combine_slots_nan_and_empty_shard():
+    """A shard whose samples all diverged has rho = inf and contributes 0."""
+    d = load_golden("drone_k128_h20.npz")
+    S, eps, lam = d["s0_S"], d["s0_noise"], float(d["lam"])
+    K, H, A = eps.shape
+    P = _slot_len(A, H)
+    good = _pack(S, eps, lam, P)
+    dead = np.zeros(P, np.float32)
+    dead[0] = np.inf
+    got = combine_slots(np.stack([good, dead]), lam, H, A)
+    np.testing.assert_allclose(got, combine_slots(good[None], lam, H, A), rtol=0, atol=0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, name, V, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d = load_golden(name)
+        S, eps, lam = d["s0_S"], d["s0_noise"], float(d["lam"])
+        K, H, A = eps.shape
+        P = _slot_len(A, H)
+        a, b = _shards(K, world)[rank]
+        # (G, V, P) zeroed exchange buffer; this rank fills only its slot.  Vehicle v
+        # sees the fixture's costs shifted by v (a different, still valid, problem).
+        buf = torch.zeros(world * V * P, dtype=torch.float32)
+        view = buf.view(world, V, P)
+        for v in range(V):
+            view[rank, v] = torch.from_numpy(_pack(S[a:b] + v, eps[a:b], lam, P))
+        mine = view[rank].clone()
+        all_reduce_slots(buf)
+        # SUM over zero padding is a gather: this rank's slot is bit-identical
+        assert torch.equal(view[rank], mine)
+        outs = [combine_slots(view[:, v].numpy(), lam, H, A) for v in range(V)]
+        q.put((rank, view.numpy().copy(), outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,V", [("arm_k100_h32_f64.npz", 1), ("wholebody_k32_h64.npz", 3)])
+def test_gloo_world2_exchange(name, V):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, V, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    # every rank ends with the same slots and the same combined w_eps
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    d = load_golden(name)
+    S, eps, lam = d["s0_S"], d["s0_noise"], float(d["lam"])
+    for v in range(V):
+        np.testing.assert_array_equal(res[0][2][v], res[1][2][v])
+        rho, eta, N = O.shard_partial(torch.as_tensor(S + v), torch.as_tensor(eps), lam)
+        want = (N / eta).numpy()
+        np.testing.assert_allclose(res[0][2][v], want, rtol=2e-5, atol=1e-6 * np.abs(want).max())
