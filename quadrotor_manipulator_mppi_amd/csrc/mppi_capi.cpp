@@ -247,10 +247,10 @@ void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xy
 // =============================================================================
 // MPPI_STAMPS diagnostics: stamp indices in program order and the phase each
 // difference measures (see the STAMP calls in mppi_rollout.hip / mppi_finalize.hip).
-static const std::vector<int> kRollStampOrder = {0, 8, 9, 10, 1, 2, 3, 4, 5, 11, 6, 12, 7};
-static const char* const kRollStampNames[] = {"", "kernarg", "loads(waited)", "philox0", "barrier", "noise",
-                                              "integrator", "fk+cost", "S+softmin", "deposit", "combine-barrier",
-                                              "fw", "record"};
+static const std::vector<int> kRollStampOrder = {0, 9, 10, 8, 1, 2, 3, 4, 5, 11, 6, 12, 7};
+static const char* const kRollStampNames[] = {"", "loads(waited)", "philox0", "lds-writes(waited)", "barrier",
+                                              "noise", "integrator", "fk+cost", "S+softmin", "deposit",
+                                              "combine-barrier", "fw", "record"};
 static const std::vector<int> kFinStampOrder = {0, 7, 8, 1, 2, 3, 4, 5, 6};
 static const char* const kFinStampNames[] = {"", "setup", "rec-loads", "min", "accum", "eta-reduce",
                                              "col-reduce", "final-col", "outputs"};

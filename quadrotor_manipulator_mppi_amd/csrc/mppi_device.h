@@ -37,17 +37,6 @@ __device__ __forceinline__ float dpp_f32(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWMASK, 0xF, false));
 }
 
-// Inclusive prefix sum inside segments of L lanes (L in {16, 32, 64}).
-__device__ __forceinline__ double seg_scan(double x, int L) {
-    x += dpp_f64<0x111, 0xF>(x);
-    x += dpp_f64<0x112, 0xF>(x);
-    x += dpp_f64<0x114, 0xF>(x);
-    x += dpp_f64<0x118, 0xF>(x);
-    if (L >= 32) x += dpp_f64<0x142, 0xA>(x);
-    if (L >= 64) x += dpp_f64<0x143, 0xC>(x);
-    return x;
-}
-
 __device__ __forceinline__ double read_lane_f64(double x, int lane) {
     int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
     int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);

@@ -207,37 +207,6 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 #define STAMPW(i) do { } while (0)
 #endif
 
-// Inclusive prefix sum in fp64 inside L-lane segments (Kogge-Stone over DPP):
-// torch's CPU cumsum accumulates fp32 inputs in double, so this reproduces its
-// fp32 outputs exactly.
-template <int L>
-__device__ __forceinline__ double seg_scan_f64(double x) {
-    x += shr_f64<0x111>(x);
-    x += shr_f64<0x112>(x);
-    x += shr_f64<0x114>(x);
-    x += shr_f64<0x118>(x);
-    if (L >= 32) x += dpp_f64<0x142, 0xA>(x);
-    if (L >= 64) x += dpp_f64<0x143, 0xC>(x);
-    return x;
-}
-
-// The same scan over NA independent dims, step-major so the DPP wait states of
-// one dim are filled by the others (explicit ILP across the A dims).
-template <int L, int NA>
-__device__ __forceinline__ void seg_scan_f64_multi(double (&x)[NA]) {
-    double y[NA];
-#define MPPI_SCAN_STEP(CALL)                                  \
-    _Pragma("unroll") for (int a = 0; a < NA; ++a) y[a] = CALL; \
-    _Pragma("unroll") for (int a = 0; a < NA; ++a) x[a] += y[a];
-    MPPI_SCAN_STEP((shr_f64<0x111>(x[a])))
-    MPPI_SCAN_STEP((shr_f64<0x112>(x[a])))
-    MPPI_SCAN_STEP((shr_f64<0x114>(x[a])))
-    MPPI_SCAN_STEP((shr_f64<0x118>(x[a])))
-    if (L >= 32) { MPPI_SCAN_STEP((dpp_f64<0x142, 0xA>(x[a]))) }
-    if (L >= 64) { MPPI_SCAN_STEP((dpp_f64<0x143, 0xC>(x[a]))) }
-#undef MPPI_SCAN_STEP
-}
-
 // Inclusive fp32 segment sum (cost reduction; order-insensitive at tolerance).
 template <int L>
 __device__ __forceinline__ float seg_scan_f32(float x) {
@@ -251,6 +220,24 @@ __device__ __forceinline__ float seg_scan_f32(float x) {
 }
 
 
+// fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
+// (the DPP wait states of one dim are filled by the others).  Each step is one
+// v_add_f32_dpp: x + dpp(x), where out-of-row sources read 0 (row_shr with
+// bound_ctrl) or rows outside row_mask add 0 (row_bcast), so no zeroing moves.
+template <int L, int NA>
+__device__ __forceinline__ void seg_scan_f32_multi(float (&x)[NA]) {
+#define MPPI_SCAN_STEP(CTRL, RM, BC)                                                    \
+    _Pragma("unroll") for (int a = 0; a < NA; ++a) x[a] += __int_as_float(             \
+        __builtin_amdgcn_update_dpp(0, __float_as_int(x[a]), CTRL, RM, 0xF, BC));
+    MPPI_SCAN_STEP(0x111, 0xF, true)
+    MPPI_SCAN_STEP(0x112, 0xF, true)
+    MPPI_SCAN_STEP(0x114, 0xF, true)
+    MPPI_SCAN_STEP(0x118, 0xF, true)
+    if (L >= 32) { MPPI_SCAN_STEP(0x142, 0xA, false) }
+    if (L >= 64) { MPPI_SCAN_STEP(0x143, 0xC, false) }
+#undef MPPI_SCAN_STEP
+}
+
 // Value of segment s's lane l, as a wave-uniform (scalar) quantity.
 template <int R>
 __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L) {
@@ -260,60 +247,85 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
     return r;
 }
 
+// The leading scalar arguments are preloaded into SGPRs at wave launch on gfx950
+// (-mllvm -amdgpu-kernarg-preload-count, build.py): the first group's Philox
+// draw and the u_prev / joint-table loads start without waiting for the
+// kernel-argument segment (its first s_load costs ~1.5k cycles).
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
-__global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
+__global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+                                                 const uint32_t step_ctr, const uint32_t k_off,
+                                                 const int32_t noise_mode, const int32_t H_arg,
+                                                 const float* __restrict__ u_prev, const DevParams pk) {
     constexpr int R = 64 / LSEG;
     constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
+    constexpr int kJW = (int)(sizeof(JointDev) * kMaxJ / 4);   // joint table, dwords
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // Scalars and (V == 1) the vehicle constants are read from the kernel
     // arguments with scalar loads (SGPR operands, no LDS latency in the hot
     // phases); the joint table and (V > 1) the vehicle block go to LDS.
     __shared__ JointDev jnt[kMaxJ];
     __shared__ VehicleConst vcv;
+    __shared__ unsigned rmin_bits;   // block min of the waves' rho (costs >= 0: uint order = float order)
     const DevParams& p = pk;
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
     STAMP(0);
-    // warm every kernel-argument cache line the hot phases touch, in one batch
-    {
-        const float* kp = (const float*)&pk;
-        float w0 = 0.0f;
-#pragma unroll
-        for (int o = 0; o < (int)((offsetof(DevParams, joints)) / 4); o += 16) w0 += kp[o];
-        asm volatile("" :: "s"(w0));
-    }
-    STAMPW(8);
-    {
-        if (MODEL != MPPI_MODEL_DRONE) {
-            const int jw = pk.nj * (int)(sizeof(JointDev) / 4);
-            const int* js = (const int*)pk.joints;
-            for (int i = tid; i < jw; i += blockDim.x) ((int*)jnt)[i] = js[i];
-        }
-        if (!VONE) {
-            const int* vs = (const int*)(pk.vc + v);
-            for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
-        }
-    }
+    // issue the global loads first (addresses need only preloaded scalars and the
+    // kernarg pointer), keep the values in registers across the Philox draw
     float* u_lds = smem;
-    const int HA = pk.H * NA;
-    for (int i = tid; i < HA; i += blockDim.x) u_lds[i] = pk.u_prev[(size_t)v * HA + i];
+    const int HA = H_arg * NA;
+    const float* usrc = u_prev + (size_t)v * HA;
+    float ur[4];
+    int jr[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + j * (int)blockDim.x;
+        ur[j] = (i < HA) ? usrc[i] : 0.0f;
+    }
+    if (MODEL != MPPI_MODEL_DRONE) {
+        const int* js = (const int*)pk.joints;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + j * (int)blockDim.x;
+            jr[j] = (i < kJW) ? js[i] : 0;
+        }
+    }
+    if (tid == 0) rmin_bits = 0x7F800000u;   // +inf
     STAMPW(9);
     // the first group's standard normals overlap the loads above
     float z0[NCH][NA];
-    if (pk.noise_mode != MPPI_NOISE_INJECTED) {
-        const int64_t kg = pk.k_offset + (int64_t)(blockIdx.x * nw + wid) * R + sub;
+    if (noise_mode != MPPI_NOISE_INJECTED) {
+        const uint32_t kg = k_off + (uint32_t)((blockIdx.x * nw + wid) * R + sub);
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
-            draw_normals<NA>(z0[c], (uint32_t)kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, pk.step_ctr, pk.seed_lo,
-                             pk.seed_hi);
+            draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, step_ctr, seed_lo, seed_hi);
     }
     STAMP(10);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + j * (int)blockDim.x;
+        if (i < HA) u_lds[i] = ur[j];
+    }
+    for (int i = tid + 4 * (int)blockDim.x; i < HA; i += blockDim.x) u_lds[i] = usrc[i];   // H*A > 2048
+    if (MODEL != MPPI_MODEL_DRONE) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = tid + j * (int)blockDim.x;
+            if (i < kJW) ((int*)jnt)[i] = jr[j];
+        }
+        for (int i = tid + 2 * (int)blockDim.x; i < kJW; i += blockDim.x) ((int*)jnt)[i] = ((const int*)pk.joints)[i];
+    }
+    if (!VONE) {
+        const int* vs = (const int*)(pk.vc + v);
+        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
+    }
+    STAMPW(8);
     lds_barrier();
     const VehicleConst& vc = VONE ? pk.vc0 : vcv;
     const float* sdiag = pk.sdiag;
-    const int H = pk.H, K = pk.K;
+    const int H = H_arg, K = pk.K;
     STAMP(1);
 
     float acc[NCH][NA];
@@ -329,14 +341,13 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
     auto group = [&](const int it) {
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
-        const uint32_t seed_lo = pk.seed_lo, seed_hi = pk.seed_hi;
         const int plane_i = K * H;
         float* traj_base = pk.traj;
         const int g = blockIdx.x + it * p.nb;
         const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
         const int kc = kval ? k : K - 1;   // clamped: every load stays in bounds
-        const int64_t kg = p.k_offset + k;
+        const uint32_t kg = k_off + (uint32_t)k;
 
         // ---- A1/A2: eps = z Sigma (device Philox) or injected; act = u_prev + eps
         float eps[NCH][NA], act[NCH][NA];
@@ -345,7 +356,7 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
             const int t = t0 + 64 * c;
             const bool val = kval && t < H;
             const int tc = (t < H) ? t : H - 1;
-            if (p.noise_mode == MPPI_NOISE_INJECTED) {
+            if (noise_mode == MPPI_NOISE_INJECTED) {
                 const float* src = p.noise_in + (((size_t)v * K + kc) * H + tc) * NA;
 #pragma unroll
                 for (int a = 0; a < NA; ++a) eps[c][a] = src[a];
@@ -355,7 +366,7 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
 #pragma unroll
                     for (int a = 0; a < NA; ++a) z[a] = z0[c][a];
                 } else {
-                    draw_normals<NA>(z, (uint32_t)kg, (uint32_t)t, (uint32_t)v, p.step_ctr, seed_lo, seed_hi);
+                    draw_normals<NA>(z, kg, (uint32_t)t, (uint32_t)v, step_ctr, seed_lo, seed_hi);
                 }
                 if (p.sigma_diag) {
 #pragma unroll
@@ -383,52 +394,44 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
         }
         if (it == 0) STAMP(2);
 
-        // ---- A3: double integrator (standard_normal_noise.py:41-48), roundings
-        //      where torch rounds; fp32 state -> fp32 positions, fp64 state
-        //      (update_joint of float64 arrays) -> fp64 positions.
+        // ---- A3: double integrator (standard_normal_noise.py:41-48).  Both cumsums
+        //      are fp32 Kogge-Stone scans over DPP: they sum small increments
+        //      (a*dt, v*dt + a*dt^2/2), so their rounding stays ~1e-10 absolute, far
+        //      below one ulp of the positions; q0 is added in the state
+        //      dtype (fp64 state -> fp64 positions, as update_joint's float64 arrays).
         float posf[NCH][NA];
         double posd[NCH][F64 ? NA : 1];
         {
 #pragma clang fp contract(off)
-            double carry1[NA], carry2[NA], lastv_d[NA];
-            float lastv_f[NA];
+            float carry1[NA], carry2[NA], lastv[NA];
 #pragma unroll
-            for (int a = 0; a < NA; ++a) { carry1[a] = 0.0; carry2[a] = 0.0; lastv_d[a] = 0.0; lastv_f[a] = 0.0f; }
+            for (int a = 0; a < NA; ++a) { carry1[a] = 0.0f; carry2[a] = 0.0f; lastv[a] = 0.0f; }
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
-                double c1[NA], c2[NA];
+                float c1[NA], c2[NA];
 #pragma unroll
-                for (int a = 0; a < NA; ++a) c1[a] = (double)(act[c][a] * p.dt);
-                seg_scan_f64_multi<LSEG, NA>(c1);
+                for (int a = 0; a < NA; ++a) c1[a] = act[c][a] * p.dt;
+                seg_scan_f32_multi<LSEG, NA>(c1);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
                     c1[a] += carry1[a];
-                    if (NCH > 1) carry1[a] = read_lane_f64(c1[a], 63);
-                    const float c1f = (float)c1[a];
+                    if (NCH > 1) carry1[a] = read_lane_f32(c1[a], 63);
                     const float h2 = (0.5f * act[c][a]) * p.dt2;
-                    if (!F64) {
-                        const float velf = c1f + vc.vel0f[a];
-                        float prev = dpp_f32<0x138, 0xF>(velf);     // wave_shr:1
-                        if (t0 == 0) prev = (c == 0) ? vc.vel0f[a] : lastv_f[a];
-                        if (NCH > 1) lastv_f[a] = read_lane_f32(velf, 63);
-                        c2[a] = (double)(prev * p.dt + h2);
-                    } else {
-                        const double vel = (double)c1f + vc.vel0[a];
-                        double prev = dpp_f64<0x138, 0xF>(vel);
-                        if (t0 == 0) prev = (c == 0) ? vc.vel0[a] : lastv_d[a];
-                        if (NCH > 1) lastv_d[a] = read_lane_f64(vel, 63);
-                        c2[a] = prev * p.dt_d + (double)h2;
-                    }
+                    const float velf = c1[a] + vc.vel0f[a];
+                    float prev = dpp_f32<0x138, 0xF>(velf);     // wave_shr:1
+                    if (t0 == 0) prev = (c == 0) ? vc.vel0f[a] : lastv[a];
+                    if (NCH > 1) lastv[a] = read_lane_f32(velf, 63);
+                    c2[a] = prev * p.dt + h2;
                 }
-                seg_scan_f64_multi<LSEG, NA>(c2);
+                seg_scan_f32_multi<LSEG, NA>(c2);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
                     c2[a] += carry2[a];
-                    if (NCH > 1) carry2[a] = read_lane_f64(c2[a], 63);
+                    if (NCH > 1) carry2[a] = read_lane_f32(c2[a], 63);
                     if (!F64) {
-                        posf[c][a] = (float)c2[a] + vc.pos0f[a];
+                        posf[c][a] = c2[a] + vc.pos0f[a];
                     } else {
-                        posd[c][a] = c2[a] + vc.pos0[a];
+                        posd[c][a] = (double)c2[a] + vc.pos0[a];
                         posf[c][a] = (float)posd[c][a];
                     }
                 }
@@ -568,13 +571,19 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     }
     STAMP(5);
 
-    // ---- cross-wave combine in LDS -> one partial record per block
-    //      LDS: [nw][4 + NCH*64*NA]; every lane (all R segments) deposits acc
+    // ---- cross-wave combine in LDS -> one partial record per block, one barrier:
+    //      rho_b via an LDS atomic min before the deposit; every record thread
+    //      rescales the 8 wave slots itself (f_w = exp(-(rho_w - rho_b)/lambda)).
+    //      LDS: [8][4 + NCH*64*NA]; every lane (all R segments) deposits acc
     float* wsh = smem + ((HA + 3) & ~3);           // always 8 wave slots (unrolled reads)
     const int wstride = 4 + NCH * 64 * NA;
     float* mine = wsh + wid * wstride;
-    if (lane == 0) { mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f; }
-    for (int i = nw * wstride + tid; i < 8 * wstride; i += blockDim.x) wsh[i] = 0.0f;   // absent waves
+    if (lane == 0) {
+        mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f;
+        if (rho_w < INFINITY) atomicMin(&rmin_bits, __float_as_uint(rho_w));
+    }
+    for (int i = nw * wstride + tid; i < 8 * wstride; i += blockDim.x)   // absent waves: rho = inf, acc = 0
+        wsh[i] = ((i - nw * wstride) % wstride == 0) ? INFINITY : 0.0f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -582,39 +591,36 @@ __global__ void __launch_bounds__(512) k_rollout(const DevParams pk) {
     STAMPW(11);
     lds_barrier();
     STAMP(6);
-    __shared__ float fw[16];
-    float rho_b = INFINITY;
-    for (int w = 0; w < nw; ++w) rho_b = fminf(rho_b, wsh[w * wstride]);
-    if (tid < 8) {
-        const float rw = (tid < nw) ? wsh[tid * wstride] : INFINITY;
-        fw[tid] = (rw == INFINITY) ? 0.0f : __expf(p.coef * (rw - rho_b));
+    const float rho_b = __uint_as_float(rmin_bits);
+    float fw[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const float rw = wsh[w * wstride];
+        fw[w] = (rw < INFINITY) ? __expf(p.coef * (rw - rho_b)) : 0.0f;
     }
-    lds_barrier();
     STAMP(12);
-    float* hb = p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4;
     if (tid == 0) {
         float eta = 0.0f, eta2 = 0.0f, nanf = 0.0f;
-        for (int w = 0; w < nw; ++w) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
             eta += fw[w] * wsh[w * wstride + 1];
             eta2 += fw[w] * fw[w] * wsh[w * wstride + 2];
             nanf = fmaxf(nanf, wsh[w * wstride + 3]);
         }
-        *reinterpret_cast<float4*>(hb) = make_float4(rho_b, eta, eta2, nanf);
+        *reinterpret_cast<float4*>(p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4) = make_float4(rho_b, eta, eta2, nanf);
     }
     // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t]
     for (int i = tid; i < HA; i += blockDim.x) {
         const int a = i / H, t = i - a * H;
         const int c = t >> 6, tl = t & 63;
-        float sw[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {   // slots of absent waves hold 0 (zeroed) and fw = 0
-            sw[w] = 0.0f;
-#pragma unroll
-            for (int sg = 0; sg < R; ++sg) sw[w] += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
-        }
         float s = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) s += fw[w] * sw[w];
+        for (int w = 0; w < 8; ++w) {
+            float sw = 0.0f;
+#pragma unroll
+            for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
+            s += fw[w] * sw;
+        }
         p.rdata[(((size_t)v * NA + a) * p.nb + blockIdx.x) * H + t] = s;
     }
     STAMP(7);
@@ -647,9 +653,11 @@ template <int MODEL, int NA, int NCH, int LSEG, bool F64>
 static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
     if (p.V == 1)
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s,
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev, p);
     else
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s, p);
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s,
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev, p);
     return (int)hipGetLastError();
 }
 
