@@ -252,8 +252,8 @@ static const char* const kRollStampNames[] = {"", "loads(waited)", "philox0", "l
                                               "noise", "integrator", "fk+cost", "S+softmin", "deposit",
                                               "combine-barrier", "fw", "record"};
 static const std::vector<int> kFinStampOrder = {0, 7, 8, 1, 2, 3, 4, 5, 6};
-static const char* const kFinStampNames[] = {"", "setup", "rec-loads", "min", "accum", "eta-reduce",
-                                             "col-reduce", "final-col", "outputs"};
+static const char* const kFinStampNames[] = {"", "loads-issued", "accum(last chunk)", "block-rho", "col-shfl",
+                                             "col-lds", "w_eps", "savgol+update", "outputs"};
 
 struct mppi_engine {
     mppi_config cfg;
@@ -658,6 +658,20 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
         for (int j = j0; fast && j < c.n_joints; ++j)
             fast = jd[j].type == MPPI_JOINT_REVOLUTE && jd[j].axis_z && jd[j].q_index == j - j0;
         p.chain_fast = fast;
+        if (fast && e->nq == 7 && c.n_joints - j0 == 7) {   // Kinova origin table (mppi_dev.h kKinova)
+            bool kin = true;
+            for (int j = 0; kin && j < 7; ++j) {
+                const float* O = jd[j0 + j].O;
+                const KinOrigin& k = kKinova[j];
+                for (int col = 0; kin && col < 3; ++col)
+                    for (int row = 0; kin && row < 3; ++row) {
+                        const float want = (row == k.p[col]) ? (float)k.s[col] : 0.0f;
+                        kin = std::fabs(O[4 * row + col] - want) <= 1e-6f;
+                    }
+                for (int d = 0; kin && d < 3; ++d) kin = ((k.tmask >> d) & 1) ? true : (O[4 * d + 3] == 0.0f);
+            }
+            if (kin && !getenv("MPPI_NO_KINOVA_PATH")) p.chain_fast = 2;
+        }
     }
     p.P = P; p.C = e->C;
     p.seed_lo = (uint32_t)c.seed; p.seed_hi = (uint32_t)(c.seed >> 32);
@@ -665,7 +679,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.dt = (float)c.dt; p.dt2 = (float)(c.dt * c.dt); p.dt_d = c.dt;
     p.coef = (float)(-1.0 / c.lambda_);
     p.w_sp = c.w_stage_pos; p.w_so = c.w_stage_ori; p.w_tp = c.w_term_pos; p.w_to = c.w_term_ori;
-    for (int j = 0; j < kMaxJ; ++j) p.joints[j] = jd[j];
+    p.joints = e->d_joints;
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS
@@ -822,7 +836,6 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         const size_t slot = (size_t)e->V * e->dp.P;
         HIP_TRY(hipMemsetAsync(e->d_exchange, 0, sizeof(float) * slot * e->cfg.shard_count, e->stream));
         FinParams f = e->fp;
-        f.vc0 = e->h_vc[0];
         f.mode = 1;
         block_records(e, f);
         f.dst = e->d_exchange + slot * e->cfg.shard_rank;
@@ -832,11 +845,12 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     return MPPI_OK;
 }
 
-mppi_status mppi_finalize(mppi_engine* e) {
-    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+// record_out: mark the outputs' completion with ev_out (read_outputs waits on it).
+// Back-to-back steps (mppi_run_steps) mark only the last one: an event record is
+// a queue packet of its own, ~1 us of device time per step.
+static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     if (use_device(e)) return MPPI_ERR_HIP;
     FinParams f = e->fp;
-    f.vc0 = e->h_vc[0];
     f.mode = 0;
     if (e->cfg.shard_count > 1) {   // slots [shard][v][P]: header then N[a][t]
         const int64_t P = e->dp.P;
@@ -851,10 +865,15 @@ mppi_status mppi_finalize(mppi_engine* e) {
     int rc = mppi_launch_finalize(&f, e->stream);
     if (rc != 0) return fail(MPPI_ERR_HIP, "finalize launch failed (%d)", rc);
     if (e->timing) { HIP_TRY(hipEventRecord(e1, e->stream)); e->fin_pairs.emplace_back(e0, e1); }
-    HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
+    if (record_out) HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
     ++e->step_ctr;
-    e->out_pending = true;
+    e->out_pending = record_out;
     return MPPI_OK;
+}
+
+mppi_status mppi_finalize(mppi_engine* e) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    return finalize_impl(e, true);
 }
 
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats) {
@@ -941,7 +960,7 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     for (int i = 0; i < n; ++i) {
         mppi_status st = mppi_rollout(e, nullptr);
         if (st != MPPI_OK) return st;
-        if ((st = mppi_finalize(e)) != MPPI_OK) return st;
+        if ((st = finalize_impl(e, i == n - 1)) != MPPI_OK) return st;
     }
     return MPPI_OK;
 }
@@ -960,7 +979,6 @@ mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, do
     p.vc0 = e->h_vc[0];
     p.step_ctr = e->step_ctr;
     FinParams f = e->fp;
-    f.vc0 = e->h_vc[0];
     f.mode = 0;
     block_records(e, f);
     float ms0 = 0.0f, ms1 = 0.0f;

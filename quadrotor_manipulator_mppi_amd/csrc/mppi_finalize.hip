@@ -2,6 +2,8 @@
 // combine the rollout blocks' partial records, w_eps, SavGol (svg_filter.py:13-90),
 // u += w_eps and the outputs (mppi.py:144-158, drone_mppi.py:157-169).  The same
 // kernel in PACK mode folds a shard's records into its exchange slot.
+#include <algorithm>
+
 #include "mppi_device.h"
 
 using namespace mppi;
@@ -16,7 +18,7 @@ using namespace mppi;
 //   FINAL: w_eps = N/eta, SavGol (symmetric pad), u += w_eps, outputs written
 //          straight into mapped pinned host memory (no D2H copy).
 // =============================================================================
-constexpr int kFinThreads = 256;
+constexpr int kFinThreads = 512;
 constexpr int kMaxRec = 4096;
 
 // DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
@@ -66,119 +68,123 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 #define FSTAMP(i) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
-    // grid (A * ts, V): block (a, slice) owns t in [t_lo, t_hi) of action dim a
-    // and reads the records' columns for that slice plus the SavGol halo -- the
-    // record reads are spread over A*ts CUs (a single CU streams ~10 B/clk).
+// Thread (g, q) of a block holds window column q (CW = 16/32/64 columns) of the
+// records g, g + rows, g + 2 rows, ... (rows = kFinThreads / CW).  Records are
+// consumed in chunks of rows*kNPT with every load of a chunk in flight; each
+// thread keeps its own running rho_t (online softmin, like the rollout), and the
+// threads are rescaled to the block rho once at the end -- one pass for any
+// record count.  The leading scalar arguments are preloaded into SGPRs
+// (-mllvm -amdgpu-kernarg-preload-count, build.py) so the first loads issue
+// without waiting for the kernel-argument segment.
+template <int CW>
+__global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restrict__ hdr_base,
+                                                          const float* __restrict__ dat_base,
+                                                          float* __restrict__ u_prev, const uint32_t nrec_H,
+                                                          const uint32_t geo, const int32_t hdr_rs,
+                                                          const int32_t d_rs, const int32_t d_as,
+                                                          const FinParams pk) {
     constexpr int NWV = kFinThreads / 64;
-    constexpr int kNPT = 16;                 // records per thread in the one-pass path
-    constexpr int kWin = 16 + 2 * 15;        // max slice + halo
-    __shared__ float nsum[kFinThreads];
-    __shared__ float wcol[kWin];
+    constexpr int ROWS = kFinThreads / CW;
+    constexpr int kNPT = 16;
+    __shared__ float colsum[NWV][CW];
+    __shared__ float wcol[CW];
     __shared__ float shm[2 * NWV];
     __shared__ double shd[2 * NWV];
     const FinParams& p = pk;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int a = blockIdx.x / p.ts, sl = blockIdx.x - a * p.ts, v = blockIdx.y;
+    const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
+    const int tsz = (int)(geo & 0xFFu), hf = (int)((geo >> 8) & 0xFFu), ts = (int)((geo >> 16) & 0xFFu);
+    const int A = (int)(geo >> 24);
+    const int a = blockIdx.x / ts, sl = blockIdx.x - a * ts, v = blockIdx.y;
     FSTAMP(0);
-    const int H = p.H, n = p.nrec, hf = p.half;
-    const int t_lo = sl * p.tsz, t_hi = min(H, t_lo + p.tsz);
-    const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1)
-    const float* hdr = p.hdr + (size_t)v * p.hdr_vs;
-    const size_t hrs = (size_t)p.hdr_rs;
-    const float* col = p.dat + (size_t)v * p.d_vs + (size_t)a * p.d_as + w0;
-    const size_t drs = (size_t)p.d_rs;
-    float* up = p.u_prev + (size_t)v * H * p.A;
-    const float uold0 = (tid == 0 && sl == 0) ? up[a] : 0.0f;   // the old u_prev[0] (mppi.py:157)
-    FSTAMP(7);
+    const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
+    const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
+    const float* hdr = hdr_base + (v ? (size_t)v * p.hdr_vs : 0);
+    const float* col = dat_base + (v ? (size_t)v * p.d_vs : 0) + (size_t)a * d_as + w0;
+    float* up = u_prev + (size_t)v * H * A;
+    // prefetch this slice's u_prev (t_lo + tid), incl. the OLD u_prev[0] (mppi.py:157)
+    const float u_old = (tid < t_hi - t_lo) ? up[(t_lo + tid) * A + a] : 0.0f;
+    const int g = tid / CW, q = tid - g * CW;
+    const bool qv = q < W;
 
-    // thread (g, q): window column q of records g, g + rows, ...
-    const int rows = kFinThreads / W;
-    const int g = tid / W, q = tid - g * W;
-    const bool active = g < rows;
-    float acc = 0.0f;
-    double eta = 0.0, eta2 = 0.0;
-    float rho, nanflag;
-    auto block_minmax = [&](float m, float nf) {
-        m = wave_min(m);
-        nf = wave_max(nf);
-        if (lane == 0) { shm[wv] = m; shm[NWV + wv] = nf; }
-        lds_barrier();
-        rho = shm[0]; nanflag = shm[NWV];
-#pragma unroll
-        for (int i = 1; i < NWV; ++i) { rho = fminf(rho, shm[i]); nanflag = fmaxf(nanflag, shm[NWV + i]); }
-    };
-    if (n <= rows * kNPT) {   // one pass: every load in flight before the reductions
+    float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
+    double eta = 0.0, eta2 = 0.0;   // counted by the q == 0 column only
+    for (int base = 0; base < n; base += ROWS * kNPT) {
         float4 hd[kNPT];
         float xv[kNPT];
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
-            const int r = g + i * rows;
-            const bool ok = active && r < n;
+            const int r = base + g + i * ROWS;
+            const bool ok = r < n;
             const size_t rr = (size_t)(ok ? r : 0);
-            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * hrs);
-            xv[i] = col[rr * drs + q];
-            if (!ok) { hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f); xv[i] = 0.0f; }
+            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (size_t)hdr_rs);
+            xv[i] = col[rr * (size_t)d_rs + (qv ? q : 0)];
+            if (!ok) hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f);
         }
-        FSTAMP(8);
-        float m = INFINITY, nf = 0.0f;
+        FSTAMP(7);
+        float m = INFINITY;
 #pragma unroll
-        for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nf = fmaxf(nf, hd[i].w); }
-        block_minmax(m, nf);
-        FSTAMP(1);
+        for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nanflag = fmaxf(nanflag, hd[i].w); }
+        if (m < INFINITY) {
+            const float rn = fminf(rho_t, m);
+            if (rho_t < INFINITY) {   // rescale the running sums to the new reference
+                const float sc = __expf(p.coef * (rho_t - rn));
+                acc *= sc;
+                eta *= (double)sc;
+                eta2 *= (double)sc * (double)sc;
+            }
+            rho_t = rn;
 #pragma unroll
-        for (int i = 0; i < kNPT; ++i) {
-            const float f = (hd[i].x == INFINITY) ? 0.0f : __expf(p.coef * (hd[i].x - rho));
-            acc = fmaf(f, xv[i], acc);
-            if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
-        }
-    } else {                  // two passes (many records)
-        float m = INFINITY, nf = 0.0f;
-        for (int r = tid; r < n; r += kFinThreads) {
-            const float4 h4 = *reinterpret_cast<const float4*>(hdr + (size_t)r * hrs);
-            m = fminf(m, h4.x);
-            nf = fmaxf(nf, h4.w);
-        }
-        FSTAMP(8);
-        block_minmax(m, nf);
-        FSTAMP(1);
-        if (active) {
-#pragma unroll 8
-            for (int r = g; r < n; r += rows) {
-                const float4 h4 = *reinterpret_cast<const float4*>(hdr + (size_t)r * hrs);
-                const float f = (h4.x == INFINITY) ? 0.0f : __expf(p.coef * (h4.x - rho));
-                acc = fmaf(f, col[(size_t)r * drs + q], acc);
-                if (q == 0) { eta += (double)f * h4.y; eta2 += (double)f * f * h4.z; }
+            for (int i = 0; i < kNPT; ++i) {
+                const float f = (hd[i].x < INFINITY) ? __expf(p.coef * (hd[i].x - rn)) : 0.0f;
+                acc = fmaf(f, xv[i], acc);
+                if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
             }
         }
+        FSTAMP(8);
     }
-    FSTAMP(2);
+    // block rho and nan flag
     {
+        const float m = wave_min(rho_t), nf = wave_max(nanflag);
+        if (lane == 0) { shm[wv] = m; shm[NWV + wv] = nf; }
+    }
+    lds_barrier();
+    float rho = shm[0];
+    nanflag = shm[NWV];
+#pragma unroll
+    for (int i = 1; i < NWV; ++i) { rho = fminf(rho, shm[i]); nanflag = fmaxf(nanflag, shm[NWV + i]); }
+    FSTAMP(1);
+    {   // rescale to the block rho, then reduce the columns: lanes q + CW*j of a wave by
+        // xor-shuffles, the waves through LDS
+        const float sc = (rho_t < INFINITY) ? __expf(p.coef * (rho_t - rho)) : 0.0f;
+        acc = (rho_t < INFINITY) ? acc * sc : 0.0f;
+        eta = (rho_t < INFINITY) ? eta * (double)sc : 0.0;
+        eta2 = (rho_t < INFINITY) ? eta2 * (double)sc * (double)sc : 0.0;
+        if (CW <= 16) acc += __shfl_xor(acc, 16);
+        if (CW <= 32) acc += __shfl_xor(acc, 32);
         const double e1 = wave_sum_f64(eta), e2 = wave_sum_f64(eta2);
+        if (lane < CW) colsum[wv][lane] = acc;
         if (lane == 0) { shd[wv] = e1; shd[NWV + wv] = e2; }
     }
-    nsum[tid] = active ? acc : 0.0f;
+    FSTAMP(2);
     lds_barrier();
     eta = shd[0]; eta2 = shd[NWV];
 #pragma unroll
     for (int i = 1; i < NWV; ++i) { eta += shd[i]; eta2 += shd[NWV + i]; }
-    FSTAMP(3);
-    int span = 1;
-    while (span < rows) span <<= 1;
-    for (int s = span >> 1; s > 0; s >>= 1) {   // log-step tree over g
-        if (active && g < s && g + s < rows) nsum[tid] += nsum[tid + s * W];
-        lds_barrier();
+    float N = 0.0f;
+    if (tid < CW) {
+#pragma unroll
+        for (int i = 0; i < NWV; ++i) N += colsum[i][tid];
     }
-    if (tid < W) wcol[tid] = nsum[tid];
-    lds_barrier();
-    FSTAMP(4);
+    FSTAMP(3);
 
     if (p.mode == 1) {   // PACK raw sums into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
         if (a == 0 && sl == 0 && tid == 0) {
             dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanflag;
         }
-        for (int t = t_lo + tid; t < t_hi; t += kFinThreads) dst[kHdr + a * H + t] = wcol[t - w0];
+        const int t = w0 + tid;
+        if (tid < W && t >= t_lo && t < t_hi) dst[kHdr + a * H + t] = N;
         return;
     }
 
@@ -186,31 +192,34 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const FinParams pk) {
     // pad (svg_filter.py:58: index -i-1 left of 0, 2H-1-i right of H-1), u += w_eps
     const float etaf = (nanflag > 0.0f) ? NAN : (float)eta;
     if (tid < W) {
-        const float w = wcol[tid] / etaf;
+        const float w = N / etaf;
         wcol[tid] = w;
         const int t = w0 + tid;
-        if (p.wraw && t >= t_lo && t < t_hi) p.wraw[((size_t)v * H + t) * p.A + a] = w;
+        if (p.wraw && t >= t_lo && t < t_hi) p.wraw[((size_t)v * H + t) * A + a] = w;
     }
     lds_barrier();
+    FSTAMP(4);
     float u0new = 0.0f;
-    for (int t = t_lo + tid; t < t_hi; t += kFinThreads) {
+    if (tid < t_hi - t_lo) {
+        const int t = t_lo + tid;
         float sm = 0.0f;
         for (int j = 0; j < p.window; ++j) {
             int idx = t + j - hf;
             idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
             sm += p.sg[j] * wcol[idx - w0];
         }
-        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * p.A + a] = sm;
-        const float un = up[t * p.A + a] + sm;
-        up[t * p.A + a] = un;
-        if (t == 0) u0new = un;
+        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * A + a] = sm;
+        const float un = u_old + sm;
+        up[t * A + a] = un;
+        u0new = un;
     }
     FSTAMP(5);
     if (sl == 0 && tid == 0) {
 #pragma clang fp contract(off)
         const float u0 = u0new;
-        p.u0[(size_t)v * p.A + a] = u0;
-        const VehicleConst& vc = (p.V == 1) ? p.vc0 : p.vc[v];
+        const float uold0 = u_old;
+        p.u0[(size_t)v * A + a] = u0;
+        const VehicleConst& vc = p.vc[v];
         double* out = p.out + (size_t)v * p.out_dim;
         const bool drone_dim = (p.model == MPPI_MODEL_DRONE) || (p.model == MPPI_MODEL_WHOLEBODY && a < 3);
         if (drone_dim) {   // drone_mppi.py:168-169
@@ -254,8 +263,21 @@ __global__ void k_weights(const float* S, const float* stats, float* w, int V, i
 }
 
 extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
-    if (p->nrec > kMaxRec || p->H > MPPI_MAX_HORIZON || p->tsz + 2 * p->half > 16 + 2 * 15) return -1;
-    hipLaunchKernelGGL(k_finalize, dim3(p->A * p->ts, p->V), dim3(kFinThreads), 0, (hipStream_t)stream, *p);
+    const int W = std::min(p->H, p->tsz + 2 * p->half);
+    if (p->nrec > kMaxRec || p->nrec <= 0 || p->H > MPPI_MAX_HORIZON || p->tsz > 255 || p->half > 255 ||
+        p->ts > 255 || p->A > 255 || W > 64)
+        return -1;
+    const uint32_t nh = (uint32_t)p->nrec | ((uint32_t)p->H << 16);
+    const uint32_t geo = (uint32_t)p->tsz | ((uint32_t)p->half << 8) | ((uint32_t)p->ts << 16) | ((uint32_t)p->A << 24);
+    const dim3 grid(p->A * p->ts, p->V), block(kFinThreads);
+    hipStream_t s = (hipStream_t)stream;
+#define MPPI_FIN_LAUNCH(CWV)                                                                              \
+    hipLaunchKernelGGL(k_finalize<CWV>, grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo,            \
+                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, *p)
+    if (W <= 16) MPPI_FIN_LAUNCH(16);
+    else if (W <= 32) MPPI_FIN_LAUNCH(32);
+    else MPPI_FIN_LAUNCH(64);
+#undef MPPI_FIN_LAUNCH
     return (int)hipGetLastError();
 }
 

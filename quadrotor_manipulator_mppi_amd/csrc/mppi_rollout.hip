@@ -136,6 +136,36 @@ __device__ __forceinline__ void sincos_joint(double q, float& s, float& c) {
     if ((qd + 1) & 2) c = -c;
 }
 
+// One Kinova joint: T <- T * [P | o] * Rz(q), P a signed permutation fixed at
+// compile time (kKinova, mppi_dev.h): the rotation part is register renaming and
+// negation (source modifiers), the translation only its nonzero components.
+template <int J>
+__device__ __forceinline__ void kin_joint(Mat34& T, const float* O, double q) {
+    constexpr KinOrigin k = kKinova[J];
+    Mat34 r;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float tr = T.m[4 * i + 3];
+        if (k.tmask & 1) tr = fmaf(T.m[4 * i + 0], O[3], tr);
+        if (k.tmask & 2) tr = fmaf(T.m[4 * i + 1], O[7], tr);
+        if (k.tmask & 4) tr = fmaf(T.m[4 * i + 2], O[11], tr);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) r.m[4 * i + j] = (k.s[j] > 0) ? T.m[4 * i + k.p[j]] : -T.m[4 * i + k.p[j]];
+        r.m[4 * i + 3] = tr;
+    }
+    float s, c;
+    sincos_joint(q, s, c);
+    const float omc = 1.0f - c, r22 = c + omc;   // Rodrigues about z (transformation_matrix.py:68-93)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float a0 = r.m[4 * i], a1 = r.m[4 * i + 1];
+        T.m[4 * i] = a0 * c + a1 * s;
+        T.m[4 * i + 1] = a1 * c - a0 * s;
+        T.m[4 * i + 2] = r.m[4 * i + 2] * r22;
+        T.m[4 * i + 3] = r.m[4 * i + 3];
+    }
+}
+
 // atan2 with octant reduction and a degree-8 odd minimax polynomial on [0,1]
 // (SLEEF atanf coefficients): ~25 ops, <= 3.5 ulp (ocml atan2f: 45 ops).
 __device__ __forceinline__ float atan2_fast(float y, float x) {
@@ -220,6 +250,22 @@ __device__ __forceinline__ float seg_scan_f32(float x) {
 }
 
 
+// Trajectory stores (every wave store instruction writes 256 contiguous bytes).
+// MPPI_TRAJ_STORE selects the cache policy (experiment knob):
+// 0 plain, 1 nontemporal, 2 write-through (sc1).
+#ifndef MPPI_TRAJ_STORE
+#define MPPI_TRAJ_STORE 0
+#endif
+__device__ __forceinline__ void traj_store(float* dst, float x) {
+#if MPPI_TRAJ_STORE == 1
+    __builtin_nontemporal_store(x, dst);
+#elif MPPI_TRAJ_STORE == 2
+    __hip_atomic_store(dst, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *dst = x;
+#endif
+}
+
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
 // (the DPP wait states of one dim are filled by the others).  Each step is one
 // v_add_f32_dpp: x + dpp(x), where out-of-row sources read 0 (row_shr with
@@ -255,7 +301,8 @@ template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
 __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
-                                                 const float* __restrict__ u_prev, const DevParams pk) {
+                                                 const float* __restrict__ u_prev,
+                                                 const JointDev* __restrict__ jtab, const DevParams pk) {
     constexpr int R = 64 / LSEG;
     constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
@@ -285,7 +332,7 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
         ur[j] = (i < HA) ? usrc[i] : 0.0f;
     }
     if (MODEL != MPPI_MODEL_DRONE) {
-        const int* js = (const int*)pk.joints;
+        const int* js = (const int*)jtab;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = tid + j * (int)blockDim.x;
@@ -315,8 +362,10 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
             const int i = tid + j * (int)blockDim.x;
             if (i < kJW) ((int*)jnt)[i] = jr[j];
         }
-        for (int i = tid + 2 * (int)blockDim.x; i < kJW; i += blockDim.x) ((int*)jnt)[i] = ((const int*)pk.joints)[i];
+        for (int i = tid + 2 * (int)blockDim.x; i < kJW; i += blockDim.x) ((int*)jnt)[i] = ((const int*)jtab)[i];
     }
+    if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize
+        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
     if (!VONE) {
         const int* vs = (const int*)(pk.vc + v);
         for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
@@ -454,7 +503,8 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
                             dz = posf[c][2] - vc.tpos[2];
                 x = dx * dx + dy * dy + dz * dz;
                 if (p.store_traj && val) {
-                    tdst[0] = posf[c][0]; tdst[plane] = posf[c][1]; tdst[2 * plane] = posf[c][2];
+                    traj_store(tdst, posf[c][0]); traj_store(tdst + plane, posf[c][1]);
+                    traj_store(tdst + 2 * plane, posf[c][2]);
                 }
             } else {
                 Mat34 T;   // base (times the folded leading fixed joints)
@@ -463,7 +513,15 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
                 if (MODEL == MPPI_MODEL_WHOLEBODY) {   // [R(rpy) | p_drone(k,t)] * M_fixed
                     T.m[3] += posf[c][0]; T.m[7] += posf[c][1]; T.m[11] += posf[c][2];
                 }
-                if (p.chain_fast) {   // nq revolute-z joints, q_index = 0..nq-1 in order
+                if (NQ == 7 && p.chain_fast == 2) {   // Kinova: origin rotations are signed permutations
+                    kin_joint<0>(T, jnt[p.j0 + 0].O, F64 ? posd[c][QOFF + 0] : (double)posf[c][QOFF + 0]);
+                    kin_joint<1>(T, jnt[p.j0 + 1].O, F64 ? posd[c][QOFF + 1] : (double)posf[c][QOFF + 1]);
+                    kin_joint<2>(T, jnt[p.j0 + 2].O, F64 ? posd[c][QOFF + 2] : (double)posf[c][QOFF + 2]);
+                    kin_joint<3>(T, jnt[p.j0 + 3].O, F64 ? posd[c][QOFF + 3] : (double)posf[c][QOFF + 3]);
+                    kin_joint<4>(T, jnt[p.j0 + 4].O, F64 ? posd[c][QOFF + 4] : (double)posf[c][QOFF + 4]);
+                    kin_joint<5>(T, jnt[p.j0 + 5].O, F64 ? posd[c][QOFF + 5] : (double)posf[c][QOFF + 5]);
+                    kin_joint<6>(T, jnt[p.j0 + 6].O, F64 ? posd[c][QOFF + 6] : (double)posf[c][QOFF + 6]);
+                } else if (p.chain_fast) {   // nq revolute-z joints, q_index = 0..nq-1 in order
 #pragma unroll
                     for (int j = 0; j < NQ; ++j) {
                         const JointDev& J = jnt[p.j0 + j];
@@ -504,9 +562,9 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
                 x = term ? pose_cost(T, vc, p.w_tp, p.w_to) : pose_cost(T, vc, p.w_sp, p.w_so);
                 if (p.store_traj && val) {
 #pragma unroll
-                    for (int a = 0; a < NA; ++a) tdst[a * plane] = posf[c][a];
+                    for (int a = 0; a < NA; ++a) traj_store(tdst + a * plane, posf[c][a]);
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) tdst[(NA + i) * plane] = T.m[i];
+                    for (int i = 0; i < 12; ++i) traj_store(tdst + (NA + i) * plane, T.m[i]);
                 }
             }
             xs[c] = val ? x : 0.0f;
@@ -654,10 +712,12 @@ static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
     if (p.V == 1)
         hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev, p);
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev,
+                           p.joints, p);
     else
         hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev, p);
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev,
+                           p.joints, p);
     return (int)hipGetLastError();
 }
 

@@ -208,6 +208,52 @@ def test_full_size_arm_properties_and_determinism():
         assert np.array_equal(a, b), "same seed must reproduce bit-for-bit"
 
 
+@pytest.mark.parametrize("model,K,H", [("arm", 4096, 32), ("wholebody", 2048, 64), ("drone", 8192, 20)])
+def test_launch_geometry_invariance(model, K, H):
+    """The result does not depend on the block geometry: 1-wave blocks (2048+
+    records -> multi-chunk finalize, several rollout groups per block) and
+    capped block counts agree with the default launch; costs are bit-identical
+    (a rollout's cost never depends on its block), the combine within fp32
+    reordering."""
+    state = {"arm": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 7,
+             "drone": [0, 0, 1, 0, 0, 0],
+             "wholebody": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 10}[model]
+    state = np.array(state, np.float64)
+    tgt = ([1.0, 2.0, 3.4], None) if model == "drone" else ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    res = []
+    for bt, nbv in [(0, 0), (64, 0), (256, 7), (512, 1)]:
+        e = _engine(model=model, n_samples=K, n_horizon=H, seed=21, block_threads=bt, blocks_per_vehicle=nbv)
+        e.set_target(*tgt)
+        out, u0, st = e.step(state)
+        res.append((e.get_costs(), e.get_u_prev(), out, st[0]))
+    S0, u_0, out0, st0 = res[0]
+    for S, u, out, st in res[1:]:
+        assert np.array_equal(S, S0), "per-rollout costs are geometry independent"
+        _close(u, u_0, rtol=1e-4, atol=1e-6, what="u_prev across geometries")
+        _close(out, out0, rtol=1e-5, atol=1e-7, what="outputs across geometries")
+        assert st.rho == st0.rho
+        assert abs(st.eta - st0.eta) <= 1e-4 * st0.eta
+
+
+def test_kinova_fast_path_matches_generic_chain(monkeypatch):
+    """The Kinova path drops the reference's float32 residuals of the origin
+    rotations (sin(pi) = -8.7e-8, cos(pi/2) = -4.4e-8); against the generic
+    chain product the EE moves by < 1e-6 and the costs by < 1e-7 relative."""
+    K, H = 1024, 32
+    state = np.array([0.1, -0.2, 1.0, 0.0, 0.0, 0.1305262, 0.9914449] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0]
+                     + [0.0] * 7, np.float64)
+    res = []
+    for disable in (False, True):
+        if disable:
+            monkeypatch.setenv("MPPI_NO_KINOVA_PATH", "1")
+        e = _engine(model="arm", n_samples=K, n_horizon=H, seed=3)
+        e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+        e.step(state)
+        res.append((e.get_trajectory()[0], e.get_costs()[0]))
+    _close(res[0][0], res[1][0], atol=1e-6, what="EE/q Kinova path vs generic")
+    _close(res[0][1], res[1][1], rtol=1e-6, what="S Kinova path vs generic")
+
+
 def test_shards_combine_like_one_engine():
     """Sample sharding: two shard engines + a host sum of their
     exchange slots == one engine over all samples (same global Philox stream)."""
