@@ -252,8 +252,8 @@ static const char* const kRollStampNames[] = {"", "loads(waited)", "philox0", "l
                                               "noise", "integrator", "fk+cost", "S+softmin", "deposit",
                                               "combine-barrier", "fw", "record"};
 static const std::vector<int> kFinStampOrder = {0, 7, 8, 1, 2, 3, 4, 5, 6};
-static const char* const kFinStampNames[] = {"", "loads-issued", "accum(last chunk)", "block-rho", "col-shfl",
-                                             "col-lds", "w_eps", "savgol+update", "outputs"};
+static const char* const kFinStampNames[] = {"", "loads-issued", "accum(last chunk)", "wave-fold", "barrier",
+                                             "combine", "w_eps", "savgol", "update+outputs"};
 
 struct mppi_engine {
     mppi_config cfg;

@@ -68,15 +68,16 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 #define FSTAMP(i) do { } while (0)
 #endif
 
-// Thread (g, q) of a block holds window column q (CW = 16/32/64 columns) of the
-// records g, g + rows, g + 2 rows, ... (rows = kFinThreads / CW).  Records are
-// consumed in chunks of rows*kNPT with every load of a chunk in flight; each
-// thread keeps its own running rho_t (online softmin, like the rollout), and the
-// threads are rescaled to the block rho once at the end -- one pass for any
-// record count.  The leading scalar arguments are preloaded into SGPRs
-// (-mllvm -amdgpu-kernarg-preload-count, build.py) so the first loads issue
-// without waiting for the kernel-argument segment.
-template <int CW>
+// Block = 8 waves.  Lane (g, q) of wave wv holds window column q (CW = 16/32/64
+// columns) of the records gr, gr + TR, gr + 2 TR, ... where gr = wv*ROWS + g is
+// its global row and TR = 8*ROWS the row count.  Records are consumed in chunks
+// of TR*kNPT with every load of a chunk in flight; each lane keeps a running
+// rho_t (online softmin, like the rollout).  Rows are folded inside each wave
+// (xor shuffles, DPP), the 8 waves through LDS behind ONE barrier, and wave 0
+// finishes alone: w_eps, SavGol by lane shuffles (WIN taps, template), u_prev,
+// outputs.
+// The leading scalar arguments are preloaded into SGPRs (build.py).
+template <int CW, int WIN>
 __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restrict__ hdr_base,
                                                           const float* __restrict__ dat_base,
                                                           float* __restrict__ u_prev, const uint32_t nrec_H,
@@ -84,12 +85,12 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
                                                           const int32_t d_rs, const int32_t d_as,
                                                           const FinParams pk) {
     constexpr int NWV = kFinThreads / 64;
-    constexpr int ROWS = kFinThreads / CW;
+    constexpr int ROWS = 64 / CW;          // rows per wave
+    constexpr int TR = NWV * ROWS;         // rows per block
     constexpr int kNPT = 16;
-    __shared__ float colsum[NWV][CW];
-    __shared__ float wcol[CW];
-    __shared__ float shm[2 * NWV];
-    __shared__ double shd[2 * NWV];
+    __shared__ float wcol[NWV][CW];
+    __shared__ float wrho[NWV], wnan[NWV];
+    __shared__ double weta[NWV], weta2[NWV];
     const FinParams& p = pk;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
@@ -102,19 +103,27 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
     const float* hdr = hdr_base + (v ? (size_t)v * p.hdr_vs : 0);
     const float* col = dat_base + (v ? (size_t)v * p.d_vs : 0) + (size_t)a * d_as + w0;
     float* up = u_prev + (size_t)v * H * A;
-    // prefetch this slice's u_prev (t_lo + tid), incl. the OLD u_prev[0] (mppi.py:157)
-    const float u_old = (tid < t_hi - t_lo) ? up[(t_lo + tid) * A + a] : 0.0f;
-    const int g = tid / CW, q = tid - g * CW;
+    const int g = lane / CW, q = lane - g * CW, gr = wv * ROWS + g;
     const bool qv = q < W;
+    // wave 0 prefetches u_prev over the window (lane q <-> t = w0 + q), incl. the OLD
+    // u_prev[0] (mppi.py:157)
+    const float u_old = (wv == 0 && q < W && g == 0) ? up[(w0 + q) * A + a] : 0.0f;
+    // and the vehicle constants the outputs need (slice 0 of each dim, lane 0)
+    float x0f = 0.0f, v0f = 0.0f;
+    double x0d = 0.0, v0d = 0.0;
+    if (tid == 0 && sl == 0) {
+        const VehicleConst& vc = p.vc[v];
+        x0f = vc.pos0f[a]; v0f = vc.vel0f[a]; x0d = vc.pos0[a]; v0d = vc.vel0[a];
+    }
 
     float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
     double eta = 0.0, eta2 = 0.0;   // counted by the q == 0 column only
-    for (int base = 0; base < n; base += ROWS * kNPT) {
+    for (int base = 0; base < n; base += TR * kNPT) {
         float4 hd[kNPT];
         float xv[kNPT];
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
-            const int r = base + g + i * ROWS;
+            const int r = base + gr + i * TR;
             const bool ok = r < n;
             const size_t rr = (size_t)(ok ? r : 0);
             hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (size_t)hdr_rs);
@@ -143,87 +152,83 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
         }
         FSTAMP(8);
     }
-    // block rho and nan flag
-    {
-        const float m = wave_min(rho_t), nf = wave_max(nanflag);
-        if (lane == 0) { shm[wv] = m; shm[NWV + wv] = nf; }
-    }
-    lds_barrier();
-    float rho = shm[0];
-    nanflag = shm[NWV];
-#pragma unroll
-    for (int i = 1; i < NWV; ++i) { rho = fminf(rho, shm[i]); nanflag = fmaxf(nanflag, shm[NWV + i]); }
-    FSTAMP(1);
-    {   // rescale to the block rho, then reduce the columns: lanes q + CW*j of a wave by
-        // xor-shuffles, the waves through LDS
-        const float sc = (rho_t < INFINITY) ? __expf(p.coef * (rho_t - rho)) : 0.0f;
-        acc = (rho_t < INFINITY) ? acc * sc : 0.0f;
-        eta = (rho_t < INFINITY) ? eta * (double)sc : 0.0;
-        eta2 = (rho_t < INFINITY) ? eta2 * (double)sc * (double)sc : 0.0;
+    {   // fold the wave: rescale every lane to the wave's rho, sum the rows
+        const float rw = wave_min(rho_t);
+        const float sc = (rho_t < INFINITY) ? __expf(p.coef * (rho_t - rw)) : 0.0f;
+        acc *= sc;
+        eta *= (double)sc;
+        eta2 *= (double)sc * (double)sc;
         if (CW <= 16) acc += __shfl_xor(acc, 16);
         if (CW <= 32) acc += __shfl_xor(acc, 32);
         const double e1 = wave_sum_f64(eta), e2 = wave_sum_f64(eta2);
-        if (lane < CW) colsum[wv][lane] = acc;
-        if (lane == 0) { shd[wv] = e1; shd[NWV + wv] = e2; }
+        const float nf = wave_max(nanflag);
+        if (lane < CW) wcol[wv][lane] = acc;
+        if (lane == 0) { wrho[wv] = rw; wnan[wv] = nf; weta[wv] = e1; weta2[wv] = e2; }
     }
-    FSTAMP(2);
+    FSTAMP(1);
     lds_barrier();
-    eta = shd[0]; eta2 = shd[NWV];
+    if (wv != 0) return;
+    FSTAMP(2);
+    // wave 0: combine the 4 waves (lane q = column q)
+    float rho = wrho[0], nanf = wnan[0];
 #pragma unroll
-    for (int i = 1; i < NWV; ++i) { eta += shd[i]; eta2 += shd[NWV + i]; }
+    for (int w = 1; w < NWV; ++w) { rho = fminf(rho, wrho[w]); nanf = fmaxf(nanf, wnan[w]); }
     float N = 0.0f;
-    if (tid < CW) {
+    eta = 0.0; eta2 = 0.0;
 #pragma unroll
-        for (int i = 0; i < NWV; ++i) N += colsum[i][tid];
+    for (int w = 0; w < NWV; ++w) {
+        const float f = (wrho[w] < INFINITY) ? __expf(p.coef * (wrho[w] - rho)) : 0.0f;
+        N = fmaf(f, (lane < CW) ? wcol[w][lane] : 0.0f, N);
+        eta += (double)f * weta[w];
+        eta2 += (double)f * f * weta2[w];
     }
     FSTAMP(3);
-
+    const int t = w0 + lane;              // this lane's time index (lanes < W)
+    const bool own = lane < W && t >= t_lo && t < t_hi;
     if (p.mode == 1) {   // PACK raw sums into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
-        if (a == 0 && sl == 0 && tid == 0) {
-            dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanflag;
+        if (a == 0 && sl == 0 && lane == 0) {
+            dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanf;
         }
-        const int t = w0 + tid;
-        if (tid < W && t >= t_lo && t < t_hi) dst[kHdr + a * H + t] = N;
+        if (own) dst[kHdr + a * H + t] = N;
         return;
     }
 
     // FINAL: w_eps = N/eta over the window, SavGol with the reference's symmetric
-    // pad (svg_filter.py:58: index -i-1 left of 0, 2H-1-i right of H-1), u += w_eps
-    const float etaf = (nanflag > 0.0f) ? NAN : (float)eta;
-    if (tid < W) {
-        const float w = N / etaf;
-        wcol[tid] = w;
-        const int t = w0 + tid;
-        if (p.wraw && t >= t_lo && t < t_hi) p.wraw[((size_t)v * H + t) * A + a] = w;
-    }
-    lds_barrier();
+    // pad (svg_filter.py:58: index -i-1 left of 0, 2H-1-i right of H-1) by lane
+    // shuffles (taps beyond the window are zero), u += w_eps
+    const float etaf = (nanf > 0.0f) ? NAN : (float)eta;
+    const float w = __fdividef(N, etaf);
+    if (p.wraw && own) p.wraw[((size_t)v * H + t) * A + a] = w;
     FSTAMP(4);
-    float u0new = 0.0f;
-    if (tid < t_hi - t_lo) {
-        const int t = t_lo + tid;
-        float sm = 0.0f;
-        for (int j = 0; j < p.window; ++j) {
-            int idx = t + j - hf;
-            idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
-            sm += p.sg[j] * wcol[idx - w0];
-        }
-        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * A + a] = sm;
-        const float un = u_old + sm;
-        up[t * A + a] = un;
-        u0new = un;
+    float sm = 0.0f;
+    auto tap = [&](int j) {
+        int idx = t + j - hf;
+        idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
+        const int src = min(max(idx - w0, 0), 63);
+        sm = fmaf(p.sg[j], __shfl(w, src), sm);
+    };
+    if constexpr (WIN > 0) {
+#pragma unroll
+        for (int j = 0; j < WIN; ++j) tap(j);
+    } else {
+        for (int j = 0; j < p.window; ++j) tap(j);
     }
     FSTAMP(5);
-    if (sl == 0 && tid == 0) {
+    const float un = u_old + sm;
+    if (own) {
+        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * A + a] = sm;
+        up[t * A + a] = un;
+    }
+    if (sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
 #pragma clang fp contract(off)
-        const float u0 = u0new;
+        const float u0 = un;
         const float uold0 = u_old;
         p.u0[(size_t)v * A + a] = u0;
-        const VehicleConst& vc = p.vc[v];
         double* out = p.out + (size_t)v * p.out_dim;
         const bool drone_dim = (p.model == MPPI_MODEL_DRONE) || (p.model == MPPI_MODEL_WHOLEBODY && a < 3);
         if (drone_dim) {   // drone_mppi.py:168-169
-            const float x0 = vc.pos0f[a], v0 = vc.vel0f[a];
+            const float x0 = x0f, v0 = v0f;
             const float xo = (x0 + v0 * p.dt) + (0.5f * u0) * p.dt2;
             const float vo = v0 + p.dt * u0;
             out[a] = xo;
@@ -235,11 +240,11 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
             const float t2 = ((0.5f * u0) * p.dt) * p.dt;
             const float t3 = u0 * p.dt;
             if (p.state_f64 && p.model == MPPI_MODEL_ARM) {
-                out[base + j] = (vc.pos0[a] + (double)t1) + (double)t2;
-                out[base + p.nq + j] = vc.vel0[a] + (double)t3;
+                out[base + j] = (x0d + (double)t1) + (double)t2;
+                out[base + p.nq + j] = v0d + (double)t3;
             } else {
-                out[base + j] = (double)((vc.pos0f[a] + t1) + t2);
-                out[base + p.nq + j] = (double)(vc.vel0f[a] + t3);
+                out[base + j] = (double)((x0f + t1) + t2);
+                out[base + p.nq + j] = (double)(v0f + t3);
             }
         }
         if (a == 0) {
@@ -247,7 +252,7 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
             st[0] = rho;
             st[1] = (float)eta;
             st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
-            st[3] = nanflag;
+            st[3] = nanf;
         }
     }
     FSTAMP(6);
@@ -271,12 +276,19 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     const uint32_t geo = (uint32_t)p->tsz | ((uint32_t)p->half << 8) | ((uint32_t)p->ts << 16) | ((uint32_t)p->A << 24);
     const dim3 grid(p->A * p->ts, p->V), block(kFinThreads);
     hipStream_t s = (hipStream_t)stream;
-#define MPPI_FIN_LAUNCH(CWV)                                                                              \
-    hipLaunchKernelGGL(k_finalize<CWV>, grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo,            \
+#define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
+    hipLaunchKernelGGL((k_finalize<CWV, WINV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo,    \
                        (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, *p)
-    if (W <= 16) MPPI_FIN_LAUNCH(16);
-    else if (W <= 32) MPPI_FIN_LAUNCH(32);
-    else MPPI_FIN_LAUNCH(64);
+#define MPPI_FIN_WIN(CWV)                                                                                 \
+    do {                                                                                                  \
+        if (p->window == 9) MPPI_FIN_LAUNCH(CWV, 9);                                                      \
+        else if (p->window == 5) MPPI_FIN_LAUNCH(CWV, 5);                                                 \
+        else MPPI_FIN_LAUNCH(CWV, 0);                                                                     \
+    } while (0)
+    if (W <= 16) MPPI_FIN_WIN(16);
+    else if (W <= 32) MPPI_FIN_WIN(32);
+    else MPPI_FIN_WIN(64);
+#undef MPPI_FIN_WIN
 #undef MPPI_FIN_LAUNCH
     return (int)hipGetLastError();
 }
