@@ -301,6 +301,7 @@ template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
 __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
+                                                 const int32_t nthr,
                                                  const float* __restrict__ u_prev,
                                                  const JointDev* __restrict__ jtab, const DevParams pk) {
     constexpr int R = 64 / LSEG;
@@ -316,7 +317,7 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
     __shared__ unsigned rmin_bits;   // block min of the waves' rho (costs >= 0: uint order = float order)
     const DevParams& p = pk;
     const int v = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;   // block size as a preloaded argument: blockDim would be an implicit-argument s_load
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
     STAMP(0);
     // issue the global loads first (addresses need only preloaded scalars and the
@@ -328,18 +329,26 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
     int jr[2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int i = tid + j * (int)blockDim.x;
+        const int i = tid + j * nthr;
         ur[j] = (i < HA) ? usrc[i] : 0.0f;
     }
     if (MODEL != MPPI_MODEL_DRONE) {
         const int* js = (const int*)jtab;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int i = tid + j * (int)blockDim.x;
+            const int i = tid + j * nthr;
             jr[j] = (i < kJW) ? js[i] : 0;
         }
     }
     if (tid == 0) rmin_bits = 0x7F800000u;   // +inf
+    // touch every kernel-argument line the hot phases read (one s_load per 64 B): they
+    // land in the scalar cache while the first group's Philox draw runs below
+    float kwarm = 0.0f;
+    {
+        const float* kp = (const float*)&pk;
+#pragma unroll
+        for (int o = 0; o < (int)(offsetof(DevParams, sigma) / 4); o += 16) kwarm += kp[o];
+    }
     STAMPW(9);
     // the first group's standard normals overlap the loads above
     float z0[NCH][NA];
@@ -350,25 +359,26 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
             draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, step_ctr, seed_lo, seed_hi);
     }
     STAMP(10);
+    asm volatile("" :: "s"(kwarm));
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int i = tid + j * (int)blockDim.x;
+        const int i = tid + j * nthr;
         if (i < HA) u_lds[i] = ur[j];
     }
-    for (int i = tid + 4 * (int)blockDim.x; i < HA; i += blockDim.x) u_lds[i] = usrc[i];   // H*A > 2048
+    for (int i = tid + 4 * nthr; i < HA; i += nthr) u_lds[i] = usrc[i];   // H*A > 2048
     if (MODEL != MPPI_MODEL_DRONE) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int i = tid + j * (int)blockDim.x;
+            const int i = tid + j * nthr;
             if (i < kJW) ((int*)jnt)[i] = jr[j];
         }
-        for (int i = tid + 2 * (int)blockDim.x; i < kJW; i += blockDim.x) ((int*)jnt)[i] = ((const int*)jtab)[i];
+        for (int i = tid + 2 * nthr; i < kJW; i += nthr) ((int*)jnt)[i] = ((const int*)jtab)[i];
     }
     if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize
-        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
+        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += nthr) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
     if (!VONE) {
         const int* vs = (const int*)(pk.vc + v);
-        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += blockDim.x) ((int*)&vcv)[i] = vs[i];
+        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += nthr) ((int*)&vcv)[i] = vs[i];
     }
     STAMPW(8);
     lds_barrier();
@@ -640,7 +650,7 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
         mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f;
         if (rho_w < INFINITY) atomicMin(&rmin_bits, __float_as_uint(rho_w));
     }
-    for (int i = nw * wstride + tid; i < 8 * wstride; i += blockDim.x)   // absent waves: rho = inf, acc = 0
+    for (int i = nw * wstride + tid; i < 8 * wstride; i += nthr)   // absent waves: rho = inf, acc = 0
         wsh[i] = ((i - nw * wstride) % wstride == 0) ? INFINITY : 0.0f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -668,7 +678,7 @@ __global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const u
         *reinterpret_cast<float4*>(p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4) = make_float4(rho_b, eta, eta2, nanf);
     }
     // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t]
-    for (int i = tid; i < HA; i += blockDim.x) {
+    for (int i = tid; i < HA; i += nthr) {
         const int a = i / H, t = i - a * H;
         const int c = t >> 6, tl = t & 63;
         float s = 0.0f;
@@ -712,12 +722,12 @@ static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
     if (p.V == 1)
         hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev,
-                           p.joints, p);
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
+                           p.u_prev, p.joints, p);
     else
         hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, p.u_prev,
-                           p.joints, p);
+                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
+                           p.u_prev, p.joints, p);
     return (int)hipGetLastError();
 }
 
