@@ -298,7 +298,7 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
 // draw and the u_prev / joint-table loads start without waiting for the
 // kernel-argument segment (its first s_load costs ~1.5k cycles).
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
-__global__ void __launch_bounds__(512) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+__global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
                                                  const int32_t nthr,
