@@ -21,9 +21,15 @@ namespace {
 // ------------------------------------------------------------------- Philox
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
                                          uint32_t k0, uint32_t k1) {
+    k0 = __builtin_amdgcn_readfirstlane(k0);   // the key is wave-uniform: keep it scalar
+    k1 = __builtin_amdgcn_readfirstlane(k1);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        if (r) {   // key schedule in place (opaque scalar adds): hoisting 18 round keys
+                   // would spill SGPRs in the rollout kernel
+            asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(k0) :: "scc");
+            asm volatile("s_add_u32 %0, %0, 0xbb67ae85" : "+s"(k1) :: "scc");
+        }
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;   // one v_mad_u64_u32 each
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
@@ -340,6 +346,10 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
             jr[j] = (i < kJW) ? js[i] : 0;
         }
     }
+    // vehicle constants -> LDS (uniform reads in the FK / cost; keeping ~60 of them
+    // in SGPRs spills): V == 1 from the kernel arguments, else from vc[v]
+    constexpr int kVCW = (int)(sizeof(VehicleConst) / 4);
+    const int vcr = (tid < kVCW) ? (VONE ? ((const int*)&pk.vc0)[tid] : ((const int*)(pk.vc + v))[tid]) : 0;
     if (tid == 0) rmin_bits = 0x7F800000u;   // +inf
     // touch every kernel-argument line the hot phases read (one s_load per 64 B): they
     // land in the scalar cache while the first group's Philox draw runs below
@@ -374,15 +384,18 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
         }
         for (int i = tid + 2 * nthr; i < kJW; i += nthr) ((int*)jnt)[i] = ((const int*)jtab)[i];
     }
-    if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize
-        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += nthr) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
-    if (!VONE) {
-        const int* vs = (const int*)(pk.vc + v);
-        for (int i = tid; i < (int)(sizeof(VehicleConst) / 4); i += nthr) ((int*)&vcv)[i] = vs[i];
+    if (tid < kVCW) {
+        ((int*)&vcv)[tid] = vcr;
+        if (VONE && blockIdx.x == 0) ((int*)pk.vc)[tid] = vcr;   // hand vc0 to the finalize
+    }
+    for (int i = tid + nthr; i < kVCW; i += nthr) {   // nthr < 124
+        const int x = VONE ? ((const int*)&pk.vc0)[i] : ((const int*)(pk.vc + v))[i];
+        ((int*)&vcv)[i] = x;
+        if (VONE && blockIdx.x == 0) ((int*)pk.vc)[i] = x;
     }
     STAMPW(8);
     lds_barrier();
-    const VehicleConst& vc = VONE ? pk.vc0 : vcv;
+    const VehicleConst& vc = vcv;
     const float* sdiag = pk.sdiag;
     const int H = H_arg, K = pk.K;
     STAMP(1);
