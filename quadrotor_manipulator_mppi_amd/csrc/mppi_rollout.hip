@@ -285,9 +285,20 @@ __device__ __forceinline__ void seg_scan_f32_multi(float (&x)[NA]) {
     MPPI_SCAN_STEP(0x112, 0xF, true)
     MPPI_SCAN_STEP(0x114, 0xF, true)
     MPPI_SCAN_STEP(0x118, 0xF, true)
-    if (L >= 32) { MPPI_SCAN_STEP(0x142, 0xA, false) }
-    if (L >= 64) { MPPI_SCAN_STEP(0x143, 0xC, false) }
 #undef MPPI_SCAN_STEP
+    // row_bcast steps as in-place v_add_f32_dpp: rows outside row_mask keep x (the
+    // compiler's DPP combiner would zero a temporary and add instead).  s_nop 1 covers
+    // the VALU-write -> DPP-read hazard the asm hides from the hazard recognizer.
+    if (L >= 32) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(x[a]));
+    }
+    if (L >= 64) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(x[a]));
+    }
 }
 
 // Value of segment s's lane l, as a wave-uniform (scalar) quantity.
@@ -486,8 +497,10 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 seg_scan_f32_multi<LSEG, NA>(c1);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
-                    c1[a] += carry1[a];
-                    if (NCH > 1) carry1[a] = read_lane_f32(c1[a], 63);
+                    if (NCH > 1) {
+                        c1[a] += carry1[a];
+                        carry1[a] = read_lane_f32(c1[a], 63);
+                    }
                     const float h2 = (0.5f * act[c][a]) * p.dt2;
                     const float velf = c1[a] + vc.vel0f[a];
                     float prev = dpp_f32<0x138, 0xF>(velf);     // wave_shr:1
@@ -498,8 +511,10 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 seg_scan_f32_multi<LSEG, NA>(c2);
 #pragma unroll
                 for (int a = 0; a < NA; ++a) {
-                    c2[a] += carry2[a];
-                    if (NCH > 1) carry2[a] = read_lane_f32(c2[a], 63);
+                    if (NCH > 1) {
+                        c2[a] += carry2[a];
+                        carry2[a] = read_lane_f32(c2[a], 63);
+                    }
                     if (!F64) {
                         posf[c][a] = c2[a] + vc.pos0f[a];
                     } else {

@@ -54,23 +54,30 @@ class ShardedEngine:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.local = int(os.environ.get("LOCAL_RANK", engine_kw.pop("device", 0)))
+        self.local %= max(1, torch.cuda.device_count())   # more ranks than devices: wrap
         torch.cuda.set_device(self.local)
         cfg = make_config(device=self.local, shard_rank=self.rank, shard_count=self.world, **engine_kw)
         self.engine = Engine(cfg)
-        self.engine.set_stream(torch.cuda.current_stream(self.local).cuda_stream)
+        # one dedicated stream carries rollout -> collective -> finalize (the default
+        # stream's handle is 0, which mppi_set_stream reads as "engine-owned stream")
+        self.stream = torch.cuda.Stream(device=self.local)
+        self.engine.set_stream(self.stream.cuda_stream)
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
         if self.world > 1:
             slot = self.engine.exchange_slot_floats()
-            self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")
+            with torch.cuda.stream(self.stream):
+                self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")
             self.engine.bind_exchange(self.buf.data_ptr())
+        self.stream.synchronize()
 
     def step_async(self, d_noise_ptr: int = 0):
-        """rollout -> (all-reduce) -> finalize, all stream-ordered, no host sync."""
-        self.engine.rollout(d_noise_ptr)
-        if self.world > 1:
-            self._exchange(self.buf, self.group)
-        self.engine.finalize()
+        """rollout -> (all-reduce) -> finalize, all ordered on self.stream, no host sync."""
+        with torch.cuda.stream(self.stream):
+            self.engine.rollout(d_noise_ptr)
+            if self.world > 1:
+                self._exchange(self.buf, self.group)
+            self.engine.finalize()
 
     def step(self, state, d_noise_ptr: int = 0):
         self.engine.set_state(state)
