@@ -22,6 +22,9 @@ Fixture map:
   rotations.npz           F4  quaternion_to_matrix (xyzw) / matrix_to_euler_angles(ZYX)
   savgol.npz              F5  SavGol coefficients and filter I/O
   wholebody_k32_h64.npz   F6  whole-body composition, 2 steps
+  arm_k64_h32_allcosts.npz F7 arm MPPI with every CostManager term the reference
+                              ships disabled (cost_manager.py:83-87) switched on,
+                              fp64 state near a joint limit, 2 steps
 """
 import contextlib
 import io
@@ -133,10 +136,34 @@ def _record_arm_step(m, seed):
     return rec
 
 
-def make_arm(path, K, H, steps, f64, seed0, state):
+def _enable_all_costs(cm, rec_terms):
+    """Switch on the terms compute_all_cost leaves commented out
+    (cost_manager.py:83-87), in that order, calling the reference's own term
+    implementations; each term's (K,) vector is recorded."""
+    def compute_all_cost():
+        S = torch.zeros((cm.n_sample), device=cm.device)
+        terms = [("stage", lambda: cm.pose_cost.compute_stage_cost(cm.eef_trajectories, cm.target)),
+                 ("terminal", lambda: cm.pose_cost.compute_terminal_cost(cm.eef_trajectories, cm.target)),
+                 ("covar", lambda: cm.covar_cost.compute_covar_cost(cm.sigma_matrix, cm.u, cm.v)),
+                 ("center", lambda: cm.joint_cost.compute_centering_cost(cm.qSamples)),
+                 ("jtraj", lambda: cm.joint_cost.compute_jointTraj_cost(cm.qSamples, cm.joint_trajectories)),
+                 ("action", lambda: cm.action_cost.compute_action_cost(cm.uSamples)),
+                 ("limit", lambda: cm.joint_cost.compute_joint_limit_cost(cm.qSamples))]
+        for name, fn in terms:
+            t = fn()
+            rec_terms[name] = _np(t)
+            S += t
+        return S
+    cm.compute_all_cost = compute_all_cost
+
+
+def make_arm(path, K, H, steps, f64, seed0, state, all_costs=False):
     with _quiet():
         m = ArmMPPI()
     _resize_arm(m, K, H)
+    terms = {}
+    if all_costs:
+        _enable_all_costs(m.cost_manager, terms)
     base, q, v_base, qd = state
     q_full = list(base) + list(q)
     v_full = list(v_base) + list(qd)
@@ -150,6 +177,8 @@ def make_arm(path, K, H, steps, f64, seed0, state):
     for s in range(steps):
         m.update_joint(q_full, v_full)
         rec = _record_arm_step(m, seed0 + s)
+        for k, val in terms.items():
+            rec[f"term_{k}"] = val
         gaps.append(_gap(rec["S"]))
         for k, val in rec.items():
             out[f"s{s}_{k}"] = val
@@ -371,6 +400,10 @@ def main():
     make_rotations(os.path.join(d, "rotations.npz"))
     make_savgol(os.path.join(d, "savgol.npz"))
     make_wholebody(os.path.join(d, "wholebody_k32_h64.npz"), 32, 64, 2, 600)
+    near_limit = ([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0],
+                  [1.57, 1.7, 0.0, 4.4, 0.0, 5.1485, 0.0],         # joint 6 2e-4 under its 5.1487 limit
+                  [0.0] * 6, [0.0, 0.3, 0.0, -0.2, 0.0, 0.0, 0.0])
+    make_arm(os.path.join(d, "arm_k64_h32_allcosts.npz"), 64, 32, 2, True, 700, near_limit, all_costs=True)
 
 
 if __name__ == "__main__":

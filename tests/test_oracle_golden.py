@@ -107,6 +107,26 @@ def test_arm_steps(kinova_chain, name):
         assert r["reach"] == bool(g[f"s{s}_reach"])
 
 
+ALL_TERMS = O.CostTerms(enabled=("covar", "center", "jtraj", "action", "limit"))
+
+
+def test_arm_all_cost_terms(kinova_chain):
+    """F7: every CostManager term the reference leaves disabled, switched on
+    (covar, centering, joint tracking, action, joint limit; cost_manager.py:83-87),
+    fp64 state near joint 6's limit so the 1e10 penalty hits some samples."""
+    g = load_golden("arm_k64_h32_allcosts.npz")
+    for s in range(int(g["steps"])):
+        r = O.arm_step(kinova_chain, g["q_full"], g["v_full"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
+                       torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"], f64=True,
+                       terms=ALL_TERMS)
+        for name in ("covar", "center", "jtraj", "action", "limit"):
+            _eq(r["terms"][name].numpy(), g[f"s{s}_term_{name}"])
+        for k in ("q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out"):
+            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+        _eq(r["qdes"], g[f"s{s}_qdes"])
+        assert (g[f"s{s}_term_limit"] > 0).any() and (g[f"s{s}_term_limit"] == 0).any()
+
+
 def test_arm_noise_reproduces_reference_randn():
     g = load_golden("arm_k32_h32_f32.npz")
     torch.manual_seed(300)
