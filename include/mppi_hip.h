@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 1
+#define MPPI_ABI_VERSION 2
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
 #define MPPI_MAX_HORIZON 256
@@ -108,7 +108,30 @@ typedef struct {
     float reach_tol;          /* 0.005                                                          */
     int32_t blocks_per_vehicle; /* rollout grid.x; 0 = auto                                     */
     int32_t block_threads;      /* rollout block size (multiple of 64); 0 = auto                */
+    /* The CostManager terms the reference ships disabled (cost_manager.py:83-87), for the
+     * ARM and WHOLEBODY models; summed after the pose terms in the reference's order
+     * (covar, centering, joint tracking, action, joint limit).  Defaults = the reference's
+     * weights (cost_manager.py:21-43, joint_space_cost.py:16,71-80). */
+    int32_t cost_terms;         /* MPPI_COST_* bits; 0 = pose cost only, as the reference runs  */
+    float w_covar;              /* covar_cost.py:20-25, scaled by lambda*(1-alpha)      (0.1)   */
+    float cost_alpha;           /* cost_manager.py:22                                   (0.1)   */
+    float cost_gamma;           /* per-step discount gamma^t of the joint/action terms  (0.98)  */
+    float w_center;             /* joint_space_cost.py:19-27                            (1.0)   */
+    float w_joint_track;        /* joint_space_cost.py:30-38 (target: mppi_set_joint_trajectory; zeros as mppi.py:134) */
+    float w_action;             /* action_cost.py:14-24 on the perturbed controls v     (0.01)  */
+    float joint_limit_penalty;  /* joint_space_cost.py:68-86                            (1e10)  */
+    float q_center[MPPI_MAX_JOINTS];   /* centering target per arm joint                         */
+    float q_lower[MPPI_MAX_JOINTS];    /* joint limits                                           */
+    float q_upper[MPPI_MAX_JOINTS];
 } mppi_config;
+
+typedef enum {
+    MPPI_COST_COVAR = 1,
+    MPPI_COST_CENTER = 2,
+    MPPI_COST_JOINT_TRACK = 4,
+    MPPI_COST_ACTION = 8,
+    MPPI_COST_JOINT_LIMIT = 16
+} mppi_cost_term;
 
 /* Per-vehicle statistics of the last finalised step. */
 typedef struct {
@@ -141,6 +164,11 @@ void mppi_destroy(mppi_engine* e);
 
 /* Run on a caller stream (hipStream_t cast to void*); NULL = engine-owned stream. */
 mppi_status mppi_set_stream(mppi_engine* e, void* hip_stream);
+
+/* Joint-space tracking target of MPPI_COST_JOINT_TRACK per vehicle: (H, nq) fp32, the
+ * joint_trajectories argument of CostManager.update_pose_cost (cost_manager.py:64-69;
+ * the reference passes zeros, mppi.py:134).  NULL restores zeros. */
+mppi_status mppi_set_joint_trajectory(mppi_engine* e, int32_t vehicle, const float* traj_h_nq);
 
 /* Goal per vehicle: position (3) and orientation quaternion xyzw (4; ignored by DRONE). */
 mppi_status mppi_set_target(mppi_engine* e, int32_t vehicle, const float* pos3, const float* quat_xyzw4);

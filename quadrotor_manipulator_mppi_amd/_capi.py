@@ -20,6 +20,8 @@ MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY = 0, 1, 2
 NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC = 0, 1, 2
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE = 0, -1, -2, -3, -4
+COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
+ABI_VERSION = 2
 
 
 class Joint(C.Structure):
@@ -40,7 +42,12 @@ class Config(C.Structure):
                 ("shard_rank", C.c_int32), ("shard_count", C.c_int32), ("state_f64", C.c_int32),
                 ("store_trajectory", C.c_int32), ("store_noise", C.c_int32),
                 ("check_reach", C.c_int32), ("reach_tol", C.c_float),
-                ("blocks_per_vehicle", C.c_int32), ("block_threads", C.c_int32)]
+                ("blocks_per_vehicle", C.c_int32), ("block_threads", C.c_int32),
+                ("cost_terms", C.c_int32), ("w_covar", C.c_float), ("cost_alpha", C.c_float),
+                ("cost_gamma", C.c_float), ("w_center", C.c_float), ("w_joint_track", C.c_float),
+                ("w_action", C.c_float), ("joint_limit_penalty", C.c_float),
+                ("q_center", C.c_float * MAX_JOINTS), ("q_lower", C.c_float * MAX_JOINTS),
+                ("q_upper", C.c_float * MAX_JOINTS)]
 
 
 class Stats(C.Structure):
@@ -69,6 +76,7 @@ PROTOTYPES = {
     "mppi_create": (_ST, [_CFG, C.POINTER(_P)]),
     "mppi_destroy": (None, [_P]),
     "mppi_set_stream": (_ST, [_P, _P]),
+    "mppi_set_joint_trajectory": (_ST, [_P, C.c_int32, _F]),
     "mppi_set_target": (_ST, [_P, C.c_int32, _F, _F]),
     "mppi_set_u_prev": (_ST, [_P, _F]),
     "mppi_get_u_prev": (_ST, [_P, _F]),
@@ -137,7 +145,7 @@ def lib():
         want = (C.sizeof(Config), C.sizeof(Joint), C.sizeof(Stats))
         if got != want:
             raise RuntimeError(f"mppi_hip ABI layout mismatch: library {got} vs binding {want}")
-        if h.mppi_abi_version() != 1:
+        if h.mppi_abi_version() != ABI_VERSION:
             raise RuntimeError("mppi_hip ABI version mismatch")
         _lib = h
         return h

@@ -280,6 +280,9 @@ struct mppi_engine {
     float* d_wraw = nullptr;
     float* d_wsmooth = nullptr;
     float* d_w = nullptr;
+    float* d_sinv = nullptr;      // extra cost terms: Sigma^-1 (A,A)
+    float* d_gamma = nullptr;     //   gamma^t (H)
+    float* d_jtraj = nullptr;     //   joint tracking target (V,H,nq)
     float* d_exchange = nullptr;
     VehicleConst* h_vc = nullptr;       // pinned staging
     unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
@@ -318,6 +321,7 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
     for (int v = 0; v < e->V; ++v) {
         VehicleConst& vc = e->h_vc[v];
         std::memset(&vc, 0, sizeof(vc));
+        for (int j = 0; j < kMaxJ; ++j) { vc.qc[j] = c.q_center[j]; vc.qlo[j] = c.q_lower[j]; vc.qhi[j] = c.q_upper[j]; }
         const double* s = e->state.data() + (size_t)v * e->state_dim;
         std::memcpy(vc.tpos, &e->tpos[3 * v], 3 * sizeof(float));
         quat_xyzw_to_R(&e->tquat[4 * v], vc.tR);
@@ -431,6 +435,9 @@ mppi_status validate(const mppi_config& c) {
     if (!(c.lambda_ > 0.0) || !(c.dt > 0.0)) return fail(MPPI_ERR_INVALID_ARG, "lambda and dt must be > 0");
     if (c.shard_count < 1 || c.shard_rank < 0 || c.shard_rank >= c.shard_count)
         return fail(MPPI_ERR_INVALID_ARG, "shard %d/%d", c.shard_rank, c.shard_count);
+    if (c.cost_terms & ~0x1F) return fail(MPPI_ERR_INVALID_ARG, "unknown cost_terms bits 0x%x", c.cost_terms);
+    if (c.cost_terms && c.model == MPPI_MODEL_DRONE)
+        return fail(MPPI_ERR_INVALID_ARG, "cost_terms apply to the ARM / WHOLEBODY CostManager (not DRONE)");
     if (c.block_threads && (c.block_threads % 64 || c.block_threads > 512))
         return fail(MPPI_ERR_INVALID_ARG, "block_threads must be a multiple of 64 <= 512");
     return MPPI_OK;
@@ -480,6 +487,19 @@ void mppi_config_default(mppi_config* c, int32_t model) {
         c->savgol_window = 9;
         c->check_reach = (model == MPPI_MODEL_ARM);
         c->state_f64 = (model == MPPI_MODEL_ARM);
+    }
+    // extra CostManager terms, off as in the reference (cost_manager.py:83-87); weights
+    // cost_manager.py:21-43, targets / limits joint_space_cost.py:16,71-72
+    c->cost_terms = 0;
+    c->w_covar = 0.1f; c->cost_alpha = 0.1f; c->cost_gamma = 0.98f;
+    c->w_center = 1.0f; c->w_joint_track = 1.0f; c->w_action = 0.01f; c->joint_limit_penalty = 1e10f;
+    const float qc[7] = {0.0f, 0.0f, 0.0f, (float)((-3.0718 - 0.0698) / 2), 0.0f, (float)((3.7525 - 0.0175) / 2), 0.0f};
+    const float lo[7] = {-6.2832f, 0.8203f, -6.2832f, 0.5236f, -6.2832f, 1.1345f, -6.2832f};
+    const float hi[7] = {6.2832f, 5.4629f, 6.2832f, 5.7596f, 6.2832f, 5.1487f, 6.2832f};
+    for (int j = 0; j < MPPI_MAX_JOINTS; ++j) {
+        c->q_center[j] = j < 7 ? qc[j] : 0.0f;
+        c->q_lower[j] = j < 7 ? lo[j] : -INFINITY;
+        c->q_upper[j] = j < 7 ? hi[j] : INFINITY;
     }
 }
 
@@ -619,6 +639,38 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     std::memset(e->h_out, 0, e->out_bytes);
     CREATE_TRY(hipMalloc(&e->d_sigma, sizeof(float) * kMaxA * kMaxA));
     CREATE_TRY(hipMemcpy(e->d_sigma, c.sigma, sizeof(float) * e->A * e->A, hipMemcpyHostToDevice));
+    if (c.cost_terms) {   // Sigma^-1 (covar_cost.py:21), gamma^t (action_cost.py:21), tracking target
+        std::vector<double> m(e->A * 2 * e->A, 0.0);
+        const int A = e->A, W2 = 2 * A;
+        for (int i = 0; i < A; ++i) {
+            for (int j = 0; j < A; ++j) m[i * W2 + j] = c.sigma[i * A + j];
+            m[i * W2 + A + i] = 1.0;
+        }
+        for (int col = 0; col < A; ++col) {   // Gauss-Jordan, partial pivoting, fp64
+            int piv = col;
+            for (int r = col + 1; r < A; ++r)
+                if (std::fabs(m[r * W2 + col]) > std::fabs(m[piv * W2 + col])) piv = r;
+            if (std::fabs(m[piv * W2 + col]) < 1e-30) { mppi_destroy(e); return fail(MPPI_ERR_INVALID_ARG, "Sigma is singular"); }
+            for (int j = 0; j < W2; ++j) std::swap(m[col * W2 + j], m[piv * W2 + j]);
+            const double d = m[col * W2 + col];
+            for (int j = 0; j < W2; ++j) m[col * W2 + j] /= d;
+            for (int r = 0; r < A; ++r)
+                if (r != col) {
+                    const double f2 = m[r * W2 + col];
+                    for (int j = 0; j < W2; ++j) m[r * W2 + j] -= f2 * m[col * W2 + j];
+                }
+        }
+        std::vector<float> sinv(A * A), gam(H);
+        for (int i = 0; i < A; ++i)
+            for (int j = 0; j < A; ++j) sinv[i * A + j] = (float)m[i * W2 + A + j];
+        for (int t = 0; t < H; ++t) gam[t] = std::pow(c.cost_gamma, (float)t);
+        CREATE_TRY(hipMalloc(&e->d_sinv, sizeof(float) * A * A));
+        CREATE_TRY(hipMalloc(&e->d_gamma, sizeof(float) * H));
+        CREATE_TRY(hipMalloc(&e->d_jtraj, sizeof(float) * (size_t)e->V * H * std::max(1, e->nq)));
+        CREATE_TRY(hipMemcpy(e->d_sinv, sinv.data(), sizeof(float) * A * A, hipMemcpyHostToDevice));
+        CREATE_TRY(hipMemcpy(e->d_gamma, gam.data(), sizeof(float) * H, hipMemcpyHostToDevice));
+        CREATE_TRY(hipMemset(e->d_jtraj, 0, sizeof(float) * (size_t)e->V * H * std::max(1, e->nq)));
+    }
     CREATE_TRY(hipHostMalloc((void**)&e->h_vc, sizeof(VehicleConst) * e->V, hipHostMallocDefault));
     CREATE_TRY(hipMemsetAsync(e->d_u_prev, 0, sizeof(float) * e->V * H * e->A, e->stream));
     CREATE_TRY(hipMemsetAsync(e->d_out, 0, e->out_bytes, e->stream));
@@ -680,6 +732,10 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.coef = (float)(-1.0 / c.lambda_);
     p.w_sp = c.w_stage_pos; p.w_so = c.w_stage_ori; p.w_tp = c.w_term_pos; p.w_to = c.w_term_ori;
     p.joints = e->d_joints;
+    p.cost_terms = c.cost_terms;
+    p.w_cov = (float)((double)c.w_covar * (c.lambda_ * (1.0 - (double)c.cost_alpha)));   // covar_cost.py:15,24
+    p.w_cen = c.w_center; p.w_jt = c.w_joint_track; p.w_act = c.w_action; p.lim_pen = c.joint_limit_penalty;
+    p.sinv = e->d_sinv; p.gamma_t = e->d_gamma; p.jtraj = e->d_jtraj;
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS
@@ -730,7 +786,8 @@ void mppi_destroy(mppi_engine* e) {
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
-                   e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w};
+                   e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
+                   e->d_sinv, e->d_gamma, e->d_jtraj};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -745,6 +802,18 @@ mppi_status mppi_set_stream(mppi_engine* e, void* s) {
     if (use_device(e)) return MPPI_ERR_HIP;
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->stream = s ? (hipStream_t)s : e->own_stream;
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_joint_trajectory(mppi_engine* e, int32_t v, const float* traj) {
+    if (!e || v < 0 || v >= e->V) return fail(MPPI_ERR_INVALID_ARG, "mppi_set_joint_trajectory: bad arguments");
+    if (!e->d_jtraj) return fail(MPPI_ERR_STATE, "engine created without cost_terms");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t n = (size_t)e->H * e->nq;
+    float* dst = e->d_jtraj + (size_t)v * n;
+    if (traj) HIP_TRY(hipMemcpyAsync(dst, traj, n * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    else HIP_TRY(hipMemsetAsync(dst, 0, n * sizeof(float), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return MPPI_OK;
 }
 

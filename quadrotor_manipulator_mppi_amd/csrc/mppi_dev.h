@@ -37,7 +37,10 @@ struct VehicleConst {
                           //      fixed joints; column 3 = R * (their translation), p(k,t) is added
     float tpos[3];        // target position
     float tR[9];          // target rotation (quaternion_to_matrix, xyzw)
-    float _pad[4];        // sizeof = 496 (16-byte multiple: keeps the dynamic LDS base aligned)
+    float _pad[4];
+    float qc[kMaxJ];      // extra cost terms (mppi_config): centering target and joint limits
+    float qlo[kMaxJ];     //   per arm joint (the same for every vehicle)
+    float qhi[kMaxJ];     // sizeof = 688 (16-byte multiple: keeps the dynamic LDS base aligned)
 };
 static_assert(sizeof(VehicleConst) % 16 == 0, "VehicleConst must be a 16-byte multiple");
 
@@ -97,6 +100,13 @@ struct DevParams {
     float* hdr;              // (V,nb,4) partial record headers: rho, eta, eta2, nan
     float* rdata;            // (V,A,nb,H) partial record bodies, dim-major
     unsigned long long* stamps;   // diagnostic s_memtime stamps per wave (MPPI_STAMPS), else null
+    // extra CostManager terms (mppi_config.cost_terms; cost_manager.py:83-87)
+    int32_t cost_terms;
+    float w_cov;                  // fp32(w_covar * lambda * (1 - alpha)) (covar_cost.py:24)
+    float w_cen, w_jt, w_act, lim_pen;
+    const float* sinv;            // (A,A) Sigma^-1, fp32
+    const float* gamma_t;         // (H) fp32 gamma^t
+    const float* jtraj;           // (V,H,nq) joint tracking target
 };
 constexpr int kStamps = 16;
 
@@ -133,6 +143,9 @@ struct FinParams {
 // launchers (mppi_kernels.hip)
 extern "C" {
 int mppi_launch_rollout(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_rollout_arm64(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_rollout_arm32(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_rollout_wb(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_finalize(const mppi::FinParams* p, void* stream);
 int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int K, float coef,
                         void* stream);

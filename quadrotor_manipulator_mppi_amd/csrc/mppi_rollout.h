@@ -1,4 +1,6 @@
-// mppi_rollout.hip -- gfx950 (CDNA4) rollout kernel of the MPPI control step.
+// mppi_rollout.h -- gfx950 (CDNA4) rollout kernel of the MPPI control step (the
+// template; instantiated per model in mppi_rollout_{drone,arm,arm32,wb}.hip so the
+// translation units compile in parallel).
 //
 //   k_rollout   one launch per step: noise draw -> double-integrator rollout ->
 //               FK chain -> per-rollout cost -> online-softmin partials.
@@ -14,6 +16,7 @@
 // chain, cost and softmin are lane-local; S_k is a segment reduction.
 // Trajectories are stored as SoA planes (V,C,K,H): every store instruction of a
 // wave writes 64 consecutive floats (256 B).
+#pragma once
 #include "mppi_device.h"
 
 namespace {
@@ -314,7 +317,7 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
 // (-mllvm -amdgpu-kernarg-preload-count, build.py): the first group's Philox
 // draw and the u_prev / joint-table loads start without waiting for the
 // kernel-argument segment (its first s_load costs ~1.5k cycles).
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC>
 __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
@@ -475,6 +478,42 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 for (int a = 0; a < NA; ++a) dst[a] = eps[c][a];
             }
         }
+        // extra CostManager terms on the controls (cost_manager.py:83,86): covar
+        // u_t^T Sigma^-1 v_t (covar_cost.py:20-25) and action w*gamma^t*||v_t||^2
+        // (action_cost.py:14-24); per lane, summed over t with the costs below
+        float ecov = 0.0f, eact = 0.0f, gts[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) gts[c] = 0.0f;
+        if (XC) {
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const int t = t0 + 64 * c;
+                const bool val = kval && t < H;
+                const int tc = (t < H) ? t : H - 1;
+                gts[c] = val ? p.gamma_t[tc] : 0.0f;
+                if (p.cost_terms & MPPI_COST_COVAR) {
+                    float qd = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) {
+                        float y = 0.0f;
+                        if (p.sigma_diag) {
+                            y = p.sinv[a * NA + a] * act[c][a];
+                        } else {
+#pragma unroll
+                            for (int b = 0; b < NA; ++b) y = fmaf(p.sinv[a * NA + b], act[c][b], y);
+                        }
+                        qd = fmaf(u_lds[tc * NA + a], y, qd);
+                    }
+                    ecov += val ? qd : 0.0f;
+                }
+                if (p.cost_terms & MPPI_COST_ACTION) {
+                    float s2 = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) s2 = fmaf(act[c][a], act[c][a], s2);
+                    eact += val ? (p.w_act * s2) * gts[c] : 0.0f;
+                }
+            }
+        }
         if (it == 0) STAMP(2);
 
         // ---- A3: double integrator (standard_normal_noise.py:41-48).  Both cumsums
@@ -528,6 +567,7 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
 
         // ---- A4-A10: FK + per-step cost, trajectory planes
         float xs[NCH];
+        float ecen = 0.0f, ejt = 0.0f, elim = 0.0f;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const int t = t0 + 64 * c;
@@ -606,6 +646,28 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 }
             }
             xs[c] = val ? x : 0.0f;
+            // extra joint-space terms (cost_manager.py:84,85,87; joint_space_cost.py)
+            if (XC && (p.cost_terms & (MPPI_COST_CENTER | MPPI_COST_JOINT_TRACK | MPPI_COST_JOINT_LIMIT))) {
+                const int tc = (t < H) ? t : H - 1;
+                const float* jt = p.jtraj ? p.jtraj + ((size_t)v * H + tc) * NQ : nullptr;
+                float sc = 0.0f, sj = 0.0f;
+                bool out = false;
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    const float qj = posf[c][QOFF + j];
+                    const float dc = qj - vc.qc[j];
+                    sc = fmaf(dc, dc, sc);
+                    const float dj = qj - (jt ? jt[j] : 0.0f);
+                    sj = fmaf(dj, dj, sj);
+                    const double qd = F64 ? posd[c][QOFF + j] : (double)qj;   // limits in the state dtype
+                    out |= (qd < (double)vc.qlo[j]) | (qd > (double)vc.qhi[j]);
+                }
+                if (val) {
+                    if (p.cost_terms & MPPI_COST_CENTER) ecen += (p.w_cen * sc) * gts[c];
+                    if (p.cost_terms & MPPI_COST_JOINT_TRACK) ejt += (p.w_jt * sj) * gts[c];
+                    if ((p.cost_terms & MPPI_COST_JOINT_LIMIT) && out) elim += p.lim_pen * gts[c];
+                }
+            }
         }
         if (it == 0) STAMP(4);
 
@@ -626,6 +688,22 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
             const float term = read_lane_f32(xt, s * LSEG + ((H - 1) & 63));
             float S = (MODEL == MPPI_MODEL_DRONE) ? (p.w_sp * stage) + (p.w_tp * term) : stage + term;
             S_seg[s] = (ks < K) ? S : INFINITY;
+        }
+        if (XC) {   // S += covar, center, jtraj, action, limit
+            float tsum[5] = {ecov, ecen, ejt, eact, elim};
+            const int bits[5] = {MPPI_COST_COVAR, MPPI_COST_CENTER, MPPI_COST_JOINT_TRACK, MPPI_COST_ACTION,
+                                 MPPI_COST_JOINT_LIMIT};
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                if (!(p.cost_terms & bits[i])) continue;
+                const float ts = seg_scan_f32<LSEG>(tsum[i]);
+#pragma unroll
+                for (int s = 0; s < R; ++s) {
+                    float add = read_lane_f32(ts, s * LSEG + LSEG - 1);
+                    if (i == 0) add = p.w_cov * add;
+                    S_seg[s] += add;
+                }
+            }
         }
         float S_mine = S_seg[0];
 #pragma unroll
@@ -722,45 +800,34 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
     STAMP(7);
 }
 
-__global__ void k_philox(uint64_t seed, uint32_t step, int veh, int64_t k0, int K, int H, int A,
-                         float* z, uint32_t* raw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= K * H) return;
-    const int k = i / H, t = i - k * H;
-    const int nj = (A + 3) / 4;
-    for (int j = 0; j < nj; ++j) {
-        uint32_t c0 = (uint32_t)(k0 + k), c1 = (uint32_t)t, c2 = ((uint32_t)veh << 8) | (uint32_t)j, c3 = step;
-        philox10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
-        uint32_t* rw = raw + ((size_t)i * nj + j) * 4;
-        rw[0] = c0; rw[1] = c1; rw[2] = c2; rw[3] = c3;
-        float n0, n1, n2, n3;
-        box_muller(c0, c1, n0, n1);
-        box_muller(c2, c3, n2, n3);
-        const float nn[4] = {n0, n1, n2, n3};
-        for (int q = 0; q < 4; ++q)
-            if (4 * j + q < A) z[(size_t)i * A + 4 * j + q] = nn[q];
-    }
-}
-
 // =============================================================================
 // launchers
 // =============================================================================
-template <int MODEL, int NA, int NCH, int LSEG, bool F64>
-static int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
+inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
     if (p.V == 1)
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true>), dim3(p.nb, p.V), dim3(threads), lds, s,
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC>), dim3(p.nb, p.V), dim3(threads), lds, s,
                            p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
                            p.u_prev, p.joints, p);
     else
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false>), dim3(p.nb, p.V), dim3(threads), lds, s,
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC>), dim3(p.nb, p.V), dim3(threads), lds, s,
                            p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
                            p.u_prev, p.joints, p);
     return (int)hipGetLastError();
 }
 
+// the extra CostManager terms get their own instantiation: their registers would
+// otherwise be reserved (and spilled) in the common pose-cost-only kernel
+template <int MODEL, int NA, int NCH, int LSEG, bool F64>
+inline int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
+    if constexpr (MODEL != MPPI_MODEL_DRONE)
+        if (p.cost_terms) return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, true>(p, threads, s);
+    return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, false>(p, threads, s);
+}
+
 template <int MODEL, int NA, bool F64>
-static int dispatch_geom(const DevParams& p, int threads, hipStream_t s) {
+inline int dispatch_geom(const DevParams& p, int threads, hipStream_t s) {
     if (p.nch == 1 && p.L == 32) return launch_rollout_t<MODEL, NA, 1, 32, F64>(p, threads, s);
     if (p.nch == 1 && p.L == 64) return launch_rollout_t<MODEL, NA, 1, 64, F64>(p, threads, s);
     if (p.nch == 2) return launch_rollout_t<MODEL, NA, 2, 64, F64>(p, threads, s);
@@ -768,27 +835,3 @@ static int dispatch_geom(const DevParams& p, int threads, hipStream_t s) {
     return -1;
 }
 
-extern "C" int mppi_launch_rollout(const DevParams* p, int threads, void* stream) {
-    hipStream_t s = (hipStream_t)stream;
-    switch (p->model) {
-        case MPPI_MODEL_DRONE:
-            if (p->A == 3) return dispatch_geom<MPPI_MODEL_DRONE, 3, false>(*p, threads, s);
-            break;
-        case MPPI_MODEL_ARM:
-            if (p->A == 7) return p->state_f64 ? dispatch_geom<MPPI_MODEL_ARM, 7, true>(*p, threads, s)
-                                               : dispatch_geom<MPPI_MODEL_ARM, 7, false>(*p, threads, s);
-            break;
-        case MPPI_MODEL_WHOLEBODY:
-            if (p->A == 10) return dispatch_geom<MPPI_MODEL_WHOLEBODY, 10, false>(*p, threads, s);
-            break;
-    }
-    return -1;
-}
-
-extern "C" int mppi_launch_philox(uint64_t seed, uint32_t step, int vehicle, int64_t k0, int K, int H, int A,
-                                  float* z, uint32_t* raw, void* stream) {
-    const int n = K * H;
-    hipLaunchKernelGGL(k_philox, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, seed, step,
-                       vehicle, k0, K, H, A, z, raw);
-    return (int)hipGetLastError();
-}

@@ -54,7 +54,13 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
                 seed: int = 0x5EED, device: int = 0, shard_rank: int = 0, shard_count: int = 1,
                 state_f64: Optional[bool] = None, store_trajectory: bool = True, store_noise: bool = False,
                 check_reach: Optional[bool] = None, reach_tol: float = 0.005, blocks_per_vehicle: int = 0,
-                block_threads: int = 0) -> capi.Config:
+                block_threads: int = 0, cost_terms=0, cost_weights: Optional[Dict[str, float]] = None
+                ) -> capi.Config:
+    """``cost_terms``: bitmask of ``capi.COST_*`` or an iterable of names among
+    ``covar, center, joint_track, action, joint_limit`` -- the CostManager terms the
+    reference ships disabled (cost_manager.py:83-87).  ``cost_weights`` overrides
+    ``w_covar, cost_alpha, cost_gamma, w_center, w_joint_track, w_action,
+    joint_limit_penalty``."""
     L = capi.lib()
     cfg = capi.Config()
     L.mppi_config_default(C.byref(cfg), MODELS[model])
@@ -95,7 +101,29 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
     cfg.reach_tol = reach_tol
     cfg.blocks_per_vehicle = blocks_per_vehicle
     cfg.block_threads = block_threads
+    cfg.cost_terms = cost_term_bits(cost_terms)
+    for k, val in (cost_weights or {}).items():
+        if k not in COST_WEIGHT_FIELDS:
+            raise ValueError(f"unknown cost weight {k!r}")
+        setattr(cfg, k, float(val))
     return cfg
+
+
+COST_TERMS = {"covar": capi.COST_COVAR, "center": capi.COST_CENTER, "joint_track": capi.COST_JOINT_TRACK,
+              "action": capi.COST_ACTION, "joint_limit": capi.COST_JOINT_LIMIT}
+COST_WEIGHT_FIELDS = ("w_covar", "cost_alpha", "cost_gamma", "w_center", "w_joint_track", "w_action",
+                      "joint_limit_penalty")
+
+
+def cost_term_bits(terms) -> int:
+    if isinstance(terms, int):
+        return terms
+    bits = 0
+    for t in terms:
+        if t not in COST_TERMS:
+            raise ValueError(f"unknown cost term {t!r} (known: {sorted(COST_TERMS)})")
+        bits |= COST_TERMS[t]
+    return bits
 
 
 class Engine:
@@ -135,6 +163,11 @@ class Engine:
         p = np.ascontiguousarray(pos, np.float32).reshape(3)
         q = None if quat is None else np.ascontiguousarray(quat, np.float32).reshape(4)
         capi.check(self._L.mppi_set_target(self._h, vehicle, capi.fptr(p), capi.fptr(q)), "set_target")
+
+    def set_joint_trajectory(self, traj=None, vehicle: int = 0):
+        """Joint tracking target (H, nq) of the joint_track cost term (None = zeros)."""
+        t = None if traj is None else np.ascontiguousarray(traj, np.float32).reshape(self.H, -1)
+        capi.check(self._L.mppi_set_joint_trajectory(self._h, vehicle, capi.fptr(t)), "set_joint_trajectory")
 
     def set_u_prev(self, u):
         u = np.ascontiguousarray(u, np.float32).reshape(self.V, self.H, self.A)

@@ -41,7 +41,12 @@ def _is_f64(x) -> bool:
 class MPPI:
     def __init__(self, n_samples: int = 100, n_horizon: int = 32, device: Optional[int] = None,
                  noise: str = "philox", seed: int = 0x5EED, urdf_path: Optional[str] = None,
-                 root_link: str = "base", end_link: str = "j2s7s300_link_7", verbose: bool = True):
+                 root_link: str = "base", end_link: str = "j2s7s300_link_7", verbose: bool = True,
+                 cost_terms=(), cost_weights=None):
+        """``cost_terms``: CostManager terms to switch on beyond the pose cost the
+        reference runs (cost_manager.py:83-87): any of ``covar, center, joint_track,
+        action, joint_limit`` (engine.COST_TERMS); ``cost_weights`` overrides their
+        weights (defaults: cost_manager.py:21-43)."""
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
         self._dev_index = device or 0
         # mppi.py:37-42
@@ -53,6 +58,7 @@ class MPPI:
         self.dt = 0.01
         self._lambda = 0.1
         self._noise, self._seed = noise, seed
+        self._cost_terms, self._cost_weights = cost_terms, cost_weights
         self.verbose = verbose
         self.chain = parse_urdf_chain(urdf_path, root_link, end_link) if urdf_path else load_chain()
         # mppi.py:45-58
@@ -83,7 +89,8 @@ class MPPI:
             e.close()
         cfg = make_config("arm", n_samples=self.n_samples, n_horizon=self.n_horizon, dt=self.dt,
                           lam=self._lambda, chain=self.chain, noise=noise, seed=self._seed,
-                          device=self._dev_index, state_f64=f64, check_reach=True)
+                          device=self._dev_index, state_f64=f64, check_reach=True,
+                          cost_terms=self._cost_terms, cost_weights=self._cost_weights)
         self._engine = Engine(cfg)
         self._engine.set_u_prev(u)
         return self._engine
