@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -270,6 +271,8 @@ struct mppi_engine {
     float* d_u_prev = nullptr;
     float* d_noise_in = nullptr;
     uint32_t step_ctr = 0;              // Philox counter word; +1 per finalized step
+    uint32_t out_seq = 0;               // completion-flag value of the step read_outputs waits for
+    bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
     float* d_S = nullptr;
@@ -315,6 +318,9 @@ mppi_status use_device(mppi_engine* e) {
 
 size_t off_u0(const mppi_engine* e) { return ((size_t)e->V * e->out_dim * sizeof(double) + 15) & ~size_t(15); }
 size_t off_stats(const mppi_engine* e) { return (off_u0(e) + (size_t)e->V * e->A * sizeof(float) + 15) & ~size_t(15); }
+// completion flags (V, A) uint32: block (a, slice 0) of vehicle v stores the step's
+// sequence number after its outputs (system-scope release); the host polls them
+size_t off_flags(const mppi_engine* e) { return off_stats(e) + (size_t)e->V * 16; }
 
 mppi_status build_vehicle_consts(mppi_engine* e) {
     const mppi_config& c = e->cfg;
@@ -631,8 +637,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
     if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * KH * e->C));
     if (c.store_noise) CREATE_TRY(hipMalloc(&e->d_noise_out, sizeof(float) * KH * e->A));
-    e->out_bytes = (int64_t)(((size_t)e->V * e->out_dim * 8 + 15) / 16 * 16 + ((size_t)e->V * e->A * 4 + 15) / 16 * 16 +
-                             (size_t)e->V * 16);
+    e->out_bytes = (int64_t)(off_flags(e) + (size_t)e->V * e->A * sizeof(uint32_t));
     CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
     CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocMapped | hipHostMallocCoherent));
     CREATE_TRY(hipHostGetDevicePointer((void**)&e->h_out_dev, e->h_out, 0));
@@ -760,8 +765,10 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     f.out = (double*)e->h_out_dev;
     f.u0 = (float*)(e->h_out_dev + off_u0(e));
     f.stats = (float*)(e->h_out_dev + off_stats(e));
+    f.flags = (uint32_t*)(e->h_out_dev + off_flags(e));
     f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.out_dim = e->out_dim;
     if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
+    e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
     f.stamps = e->d_fstamps;
     *out = e;
     return MPPI_OK;
@@ -921,6 +928,8 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     if (use_device(e)) return MPPI_ERR_HIP;
     FinParams f = e->fp;
     f.mode = 0;
+    f.seq = e->step_ctr + 1u;   // never 0 (the flags start zeroed) unless the counter wraps
+    if (f.seq == 0u) f.seq = 1u;
     if (e->cfg.shard_count > 1) {   // slots [shard][v][P]: header then N[a][t]
         const int64_t P = e->dp.P;
         f.nrec = e->cfg.shard_count;
@@ -934,6 +943,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     int rc = mppi_launch_finalize(&f, e->stream);
     if (rc != 0) return fail(MPPI_ERR_HIP, "finalize launch failed (%d)", rc);
     if (e->timing) { HIP_TRY(hipEventRecord(e1, e->stream)); e->fin_pairs.emplace_back(e0, e1); }
+    if (record_out) e->out_seq = f.seq;
     if (record_out) HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
     ++e->step_ctr;
     e->out_pending = record_out;
@@ -945,11 +955,42 @@ mppi_status mppi_finalize(mppi_engine* e) {
     return finalize_impl(e, true);
 }
 
+// Wait for the finalised step's outputs.  k_finalize writes them into mapped
+// host memory and then, per (vehicle, dim) block, the step's sequence number
+// (after a system-scope fence), so the host sees completion by polling host
+// memory instead of waking on the output event (which also trails the kernel by
+// one queue packet).  The event stays the backstop: it is queried every few
+// hundred polls, which also surfaces a faulted queue as an error.
+static mppi_status wait_outputs(mppi_engine* e) {
+    if (!e->event_wait) {
+        const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
+        const int n = e->V * e->A;
+        const uint32_t want = e->out_seq;
+        for (uint64_t it = 1;; ++it) {
+            int j = 0;
+            while (j < n && fl[j] == want) ++j;
+            if (j == n) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                return MPPI_OK;
+            }
+            if ((it & 255u) == 0) {
+                const hipError_t q = hipEventQuery(e->ev_out);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) return fail(MPPI_ERR_HIP, "waiting for the step: %s", hipGetErrorString(q));
+            }
+            __builtin_ia32_pause();
+        }
+    }
+    HIP_TRY(hipEventSynchronize(e->ev_out));
+    return MPPI_OK;
+}
+
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (!e->out_pending) return fail(MPPI_ERR_STATE, "no finalised step to read");
     if (use_device(e)) return MPPI_ERR_HIP;
-    HIP_TRY(hipEventSynchronize(e->ev_out));
+    {   mppi_status st = wait_outputs(e);
+        if (st != MPPI_OK) return st; }
     if (e->d_stamps) {   // diagnostic: average phase cycles over all waves
         const size_t nwaves = (size_t)e->V * e->dp.nb * (e->threads / 64);
         std::vector<unsigned long long> st(nwaves * kStamps);

@@ -131,6 +131,8 @@ struct FinParams {
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)
     float* u0;               // (V, A)         -- "
     float* stats;            // (V, 4): rho, eta, ess, nonfinite -- "
+    uint32_t* flags;         // (V, A) completion flags      -- " (seq stored after the outputs)
+    uint32_t seq;            // this step's completion-flag value (never 0)
     float* wraw;             // (V,H,A) readback
     float* wsmooth;          // (V,H,A) readback
     int32_t out_dim;

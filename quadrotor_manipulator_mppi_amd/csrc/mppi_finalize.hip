@@ -254,6 +254,9 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
             st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
             st[3] = nanf;
         }
+        // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs)
+        __threadfence_system();
+        __hip_atomic_store(p.flags + (size_t)v * A + a, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     FSTAMP(6);
 }
