@@ -145,7 +145,8 @@ def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=Tru
     w = dict(WORKLOADS[name])
     w.pop("desc")
     V = w.get("n_vehicles", 1)
-    se = ShardedEngine(seed=1234, **w)
+    native = None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False
+    se = ShardedEngine(seed=1234, native=native, **w)
     eng = se.engine
     set_targets(eng, w["model"], V)
     state = make_state(w["model"], V)
@@ -157,11 +158,9 @@ def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=Tru
         torch.cuda.synchronize()
 
     def steps(n):
-        if world == 1:
-            eng.run_steps(n)          # one C call launches n control steps
-        else:
-            for _ in range(n):        # rollout -> all-reduce (RCCL) -> finalize
-                se.step_async()
+        # one C call enqueues n control steps (rollout -> all-reduce over the engine's
+        # RCCL communicator -> finalize when sharded); the gloo rehearsal path loops in Python
+        se.run_steps(n)
 
     steps(warmup)
     barrier()

@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 2
+#define MPPI_ABI_VERSION 3
+#define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
 #define MPPI_MAX_HORIZON 256
@@ -52,7 +53,8 @@ typedef enum {
     MPPI_ERR_INVALID_ARG = -1,
     MPPI_ERR_HIP = -2,
     MPPI_ERR_NONFINITE = -3,
-    MPPI_ERR_STATE = -4
+    MPPI_ERR_STATE = -4,
+    MPPI_ERR_COMM = -5
 } mppi_status;
 
 /* Rollout models.  A = action dimension. */
@@ -188,14 +190,28 @@ mppi_status mppi_set_state(mppi_engine* e, const double* state);
 mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step);
 
 /* Split-phase step (async, stream ordered).  d_noise: device eps (V,K,H,A) in
- * INJECTED mode, else NULL.  With shard_count > 1 bind an exchange buffer of
- * shard_count*V*slot floats (zeroed and filled with this shard's slot by
- * mppi_rollout); the caller sums it across shards (one all-reduce), then calls
- * mppi_finalize. */
+ * INJECTED mode, else NULL.  With shard_count > 1 either bind a zero-initialised
+ * exchange buffer of shard_count*V*slot floats (mppi_rollout writes this shard's
+ * slot and zeroes the others at the same positions); the caller sums it across
+ * shards (one all-reduce), then calls mppi_finalize -- or let the engine own the
+ * collective (mppi_comm_init below). */
 mppi_status mppi_exchange_slot_floats(mppi_engine* e, int64_t* slot_floats);
 mppi_status mppi_bind_exchange(mppi_engine* e, float* d_exchange);
 mppi_status mppi_rollout(mppi_engine* e, const float* d_noise);
 mppi_status mppi_finalize(mppi_engine* e);
+
+/* Native collective: one process per GPU, one engine per process.
+ * Rank 0 makes an id, the caller broadcasts it (torch.distributed), and every rank
+ * calls mppi_comm_init with it (collective, blocking); rank/world are the config's
+ * shard_rank/shard_count.  The engine then owns an RCCL communicator over xGMI and
+ * its zero-padded (shard_count, V, slot) exchange buffer, and mppi_step /
+ * mppi_run_steps run rollout -> pack -> ONE all-reduce(SUM) -> finalize on the engine
+ * stream with no host round trip.  mppi_exchange is that all-reduce alone (split
+ * phases).  A one-rank communicator runs the same sharded path on one GPU.  The
+ * reference has no distributed code (mppi.py:31 pins one device). */
+mppi_status mppi_comm_unique_id(uint8_t id[MPPI_COMM_ID_BYTES]);
+mppi_status mppi_comm_init(mppi_engine* e, const uint8_t id[MPPI_COMM_ID_BYTES]);
+mppi_status mppi_exchange(mppi_engine* e);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles
  *   DRONE: x_des(3) v_des(3);  ARM: qdes(nq) vdes(nq);  WHOLEBODY: x(3) v(3) qdes(nq) vdes(nq)
@@ -203,12 +219,14 @@ mppi_status mppi_finalize(mppi_engine* e);
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats);
 
 /* One whole control step: set_state, (upload host noise), rollout, finalize, read_outputs.
- * h_noise: host eps (V,K,H,A) in INJECTED mode, else NULL.  Single-shard only. */
+ * h_noise: host eps (V,K,H,A) in INJECTED mode, else NULL.  Single-shard, or a
+ * shard with an engine-owned communicator. */
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out,
                       float* u0, mppi_stats* stats);
 
 /* n back-to-back asynchronous control steps (rollout + finalize each, device
- * noise, state and warm start resident on the GPU); single-shard engines only.
+ * noise, state and warm start resident on the GPU); single-shard engines, or
+ * shards with an engine-owned communicator (rollout, all-reduce, finalize).
  * No host synchronisation: pair with mppi_synchronize / mppi_read_outputs. */
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 

@@ -19,9 +19,10 @@ MAX_ACTION, MAX_JOINTS, MAX_HORIZON, MAX_SAVGOL = 16, 16, 256, 31
 MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY = 0, 1, 2
 NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC = 0, 1, 2
-OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE = 0, -1, -2, -3, -4
+OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 2
+ABI_VERSION = 3
+COMM_ID_BYTES = 128
 
 
 class Joint(C.Structure):
@@ -86,6 +87,9 @@ PROTOTYPES = {
     "mppi_bind_exchange": (_ST, [_P, _P]),
     "mppi_rollout": (_ST, [_P, _P]),
     "mppi_finalize": (_ST, [_P]),
+    "mppi_comm_unique_id": (_ST, [C.POINTER(C.c_uint8)]),
+    "mppi_comm_init": (_ST, [_P, C.POINTER(C.c_uint8)]),
+    "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),
     "mppi_step": (_ST, [_P, _D, _F, _D, _F, C.POINTER(Stats)]),
     "mppi_run_steps": (_ST, [_P, C.c_int32]),

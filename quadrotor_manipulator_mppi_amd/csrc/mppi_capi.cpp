@@ -4,7 +4,9 @@
 // the step), bakes the per-joint / per-vehicle fp32 constants exactly the way
 // the reference builds its tensors, and sequences the two kernels of a step on
 // one HIP stream.  See DESIGN.md for the data layout and the kernel roofline.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -23,6 +25,38 @@ using namespace mppi;
 namespace {
 
 thread_local std::string g_err;
+
+// RCCL, resolved at the first mppi_comm_* call (dlopen: the library loads and its
+// single-GPU paths run without RCCL; inside a torch process this binds the
+// librccl.so.1 torch already loaded, so there is one RCCL per process).
+struct Rccl {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char* (*err)(ncclResult_t) = nullptr;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW);
+        if (!h) { x.why = dlerror() ? dlerror() : "librccl.so.1 not found"; return x; }
+        x.get_unique_id = (decltype(x.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        x.init_rank = (decltype(x.init_rank))dlsym(h, "ncclCommInitRank");
+        x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
+        x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+        x.err = (decltype(x.err))dlsym(h, "ncclGetErrorString");
+        x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.err;
+        if (!x.ok) x.why = "librccl.so.1 lacks an nccl* entry point";
+        return x;
+    }();
+    return r;
+}
 
 mppi_status fail(mppi_status st, const char* fmt, ...) {
     char buf[512];
@@ -287,6 +321,8 @@ struct mppi_engine {
     float* d_gamma = nullptr;     //   gamma^t (H)
     float* d_jtraj = nullptr;     //   joint tracking target (V,H,nq)
     float* d_exchange = nullptr;
+    ncclComm_t comm = nullptr;          // engine-owned RCCL communicator (mppi_comm_init)
+    float* d_xown = nullptr;            // its exchange buffer (shard_count * V * P floats)
     VehicleConst* h_vc = nullptr;       // pinned staging
     unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
     unsigned char* h_out_dev = nullptr; // device view of h_out
@@ -310,6 +346,10 @@ struct mppi_engine {
 };
 
 namespace {
+
+// the step goes through the exchange slots: several shards, or an engine-owned
+// communicator (a one-rank communicator runs the same pack -> all-reduce -> combine)
+bool sharded(const mppi_engine* e) { return e->cfg.shard_count > 1 || e->comm; }
 
 mppi_status use_device(mppi_engine* e) {
     HIP_TRY(hipSetDevice(e->cfg.device));
@@ -792,9 +832,10 @@ void mppi_destroy(mppi_engine* e) {
     for (auto& pr : e->roll_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->comm) rccl().destroy(e->comm);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -874,7 +915,61 @@ mppi_status mppi_exchange_slot_floats(mppi_engine* e, int64_t* n) {
 
 mppi_status mppi_bind_exchange(mppi_engine* e, float* d) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (e->comm) return fail(MPPI_ERR_STATE, "the engine owns a communicator and its exchange buffer");
     e->d_exchange = d;
+    return MPPI_OK;
+}
+
+mppi_status mppi_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(MPPI_ERR_INVALID_ARG, "null id");
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(MPPI_ERR_COMM, "RCCL unavailable: %s", r.why.c_str());
+    static_assert(sizeof(ncclUniqueId) == MPPI_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    const ncclResult_t rc = r.get_unique_id(&u);
+    if (rc != ncclSuccess) return fail(MPPI_ERR_COMM, "ncclGetUniqueId: %s", r.err(rc));
+    std::memcpy(id, &u, sizeof(u));
+    return MPPI_OK;
+}
+
+// Collective over all shard engines (one per process and GPU): every rank calls it
+// with the same id, rank = cfg.shard_rank, world = cfg.shard_count.  Blocks until all
+// ranks have joined.  The engine then owns the exchange buffer and runs the per-step
+// all-reduce itself (mppi_exchange; inside mppi_step / mppi_run_steps).
+mppi_status mppi_comm_init(mppi_engine* e, const uint8_t* id) {
+    if (!e || !id) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (e->comm) return fail(MPPI_ERR_STATE, "communicator already initialised");
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(MPPI_ERR_COMM, "RCCL unavailable: %s", r.why.c_str());
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t n = (size_t)e->cfg.shard_count * e->V * e->dp.P;
+    HIP_TRY(hipMalloc(&e->d_xown, n * sizeof(float)));
+    HIP_TRY(hipMemsetAsync(e->d_xown, 0, n * sizeof(float), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t rc = r.init_rank(&e->comm, e->cfg.shard_count, u, e->cfg.shard_rank);
+    if (rc != ncclSuccess) {
+        e->comm = nullptr;
+        (void)hipFree(e->d_xown);
+        e->d_xown = nullptr;
+        return fail(MPPI_ERR_COMM, "ncclCommInitRank(rank %d of %d): %s", e->cfg.shard_rank, e->cfg.shard_count,
+                    r.err(rc));
+    }
+    e->d_exchange = e->d_xown;
+    return MPPI_OK;
+}
+
+// The step's one collective: SUM all-reduce of the zero-padded slots on the engine
+// stream, between mppi_rollout (which packed this shard's slot) and mppi_finalize.
+mppi_status mppi_exchange(mppi_engine* e) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->comm) return fail(MPPI_ERR_STATE, "mppi_exchange needs mppi_comm_init");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t n = (size_t)e->cfg.shard_count * e->V * e->dp.P;
+    const ncclResult_t rc = rccl().all_reduce(e->d_exchange, e->d_exchange, n, ncclFloat32, ncclSum, e->comm,
+                                              e->stream);
+    if (rc != ncclSuccess) return fail(MPPI_ERR_COMM, "ncclAllReduce: %s", rccl().err(rc));
     return MPPI_OK;
 }
 
@@ -891,8 +986,8 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_rollout before mppi_set_state");
     if (e->cfg.noise_mode == MPPI_NOISE_INJECTED && !d_noise)
         return fail(MPPI_ERR_INVALID_ARG, "INJECTED noise mode needs a device noise buffer");
-    if (e->cfg.shard_count > 1 && !e->d_exchange)
-        return fail(MPPI_ERR_STATE, "shard_count > 1 needs mppi_bind_exchange");
+    if (sharded(e) && !e->d_exchange)
+        return fail(MPPI_ERR_STATE, "shard_count > 1 needs mppi_bind_exchange or mppi_comm_init");
     if (use_device(e)) return MPPI_ERR_HIP;
     DevParams p = e->dp;
     p.noise_in = d_noise;
@@ -908,13 +1003,14 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         e->roll_pairs.emplace_back(e0, e1);
         if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
     }
-    if (e->cfg.shard_count > 1) {   // fold this shard's block records into its exchange slot
+    if (sharded(e)) {   // fold this shard's block records into its exchange slot
         const size_t slot = (size_t)e->V * e->dp.P;
-        HIP_TRY(hipMemsetAsync(e->d_exchange, 0, sizeof(float) * slot * e->cfg.shard_count, e->stream));
         FinParams f = e->fp;
         f.mode = 1;
         block_records(e, f);
         f.dst = e->d_exchange + slot * e->cfg.shard_rank;
+        f.xbase = e->d_exchange; f.xslot = (int64_t)slot;
+        f.nslots = e->cfg.shard_count; f.myslot = e->cfg.shard_rank;
         rc = mppi_launch_finalize(&f, e->stream);
         if (rc != 0) return fail(MPPI_ERR_HIP, "pack launch failed (%d)", rc);
     }
@@ -930,7 +1026,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     f.mode = 0;
     f.seq = e->step_ctr + 1u;   // never 0 (the flags start zeroed) unless the counter wraps
     if (f.seq == 0u) f.seq = 1u;
-    if (e->cfg.shard_count > 1) {   // slots [shard][v][P]: header then N[a][t]
+    if (sharded(e)) {   // slots [shard][v][P]: header then N[a][t]
         const int64_t P = e->dp.P;
         f.nrec = e->cfg.shard_count;
         f.hdr = e->d_exchange; f.hdr_vs = P; f.hdr_rs = (int64_t)e->V * P;
@@ -1046,7 +1142,8 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out, float* u0,
                       mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
-    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_step is single-shard; use the split phases");
+    if (sharded(e) && !e->comm)
+        return fail(MPPI_ERR_STATE, "mppi_step on a shard needs mppi_comm_init (or use the split phases)");
     mppi_status st;
     if (state && (st = mppi_set_state(e, state)) != MPPI_OK) return st;
     const float* dn = nullptr;
@@ -1059,17 +1156,19 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         dn = e->d_noise_in;
     }
     if ((st = mppi_rollout(e, dn)) != MPPI_OK) return st;
+    if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
     if ((st = mppi_finalize(e)) != MPPI_OK) return st;
     return mppi_read_outputs(e, out, u0, stats);
 }
 
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     if (!e || n < 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_run_steps: bad arguments");
-    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_run_steps is single-shard");
+    if (sharded(e) && !e->comm) return fail(MPPI_ERR_STATE, "mppi_run_steps on a shard needs mppi_comm_init");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_run_steps needs device noise");
     for (int i = 0; i < n; ++i) {
         mppi_status st = mppi_rollout(e, nullptr);
         if (st != MPPI_OK) return st;
+        if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
         if ((st = finalize_impl(e, i == n - 1)) != MPPI_OK) return st;
     }
     return MPPI_OK;
@@ -1077,7 +1176,7 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
 
 mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
     if (!e || n <= 0 || !rollout_us || !finalize_us) return fail(MPPI_ERR_INVALID_ARG, "mppi_kernel_timing: bad arguments");
-    if (e->cfg.shard_count != 1) return fail(MPPI_ERR_STATE, "mppi_kernel_timing is single-shard");
+    if (sharded(e)) return fail(MPPI_ERR_STATE, "mppi_kernel_timing is single-shard");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_kernel_timing needs device noise");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_kernel_timing before mppi_set_state");
     if (use_device(e)) return MPPI_ERR_HIP;

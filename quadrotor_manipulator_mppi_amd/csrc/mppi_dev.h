@@ -126,6 +126,9 @@ struct FinParams {
     double dt_d;
     float sg[kMaxW];         // SavGol taps (already flipped for the correlation)
     float* dst;              // pack destination (slot base, vehicle stride P)
+    float* xbase;            // pack: exchange buffer base; the other shards' slots are zeroed at
+    int64_t xslot;           //   the same positions (slot stride xslot floats), so the SUM
+    int32_t nslots, myslot;  //   all-reduce needs no memset first
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

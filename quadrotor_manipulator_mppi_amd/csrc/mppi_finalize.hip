@@ -191,6 +191,12 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
             dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanf;
         }
         if (own) dst[kHdr + a * H + t] = N;
+        for (int s = 0; s < p.nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
+            if (s == p.myslot) continue;
+            float* z = p.xbase + (size_t)s * p.xslot + (size_t)v * p.P;
+            if (a == 0 && sl == 0 && lane < kHdr) z[lane] = 0.0f;
+            if (own) z[kHdr + a * H + t] = 0.0f;
+        }
         return;
     }
 

@@ -22,6 +22,14 @@
 namespace {
 
 // ------------------------------------------------------------------- Philox
+// a ^ b ^ k in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96 (three-input
+// XOR).  The compiler emits two v_xor_b32 for it (there is no v_xor3 on gfx950).
+__device__ __forceinline__ uint32_t xor3_sk(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
                                          uint32_t k0, uint32_t k1) {
     k0 = __builtin_amdgcn_readfirstlane(k0);   // the key is wave-uniform: keep it scalar
@@ -35,9 +43,13 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
         }
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;   // one v_mad_u64_u32 each
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n0 = xor3_sk((uint32_t)(p1 >> 32), c1, k0), n2 = xor3_sk((uint32_t)(p0 >> 32), c3, k1);
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     }
+}
+
+__device__ __forceinline__ float uniform_f32(float x) {   // wave-uniform value kept in an SGPR
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
 
 __device__ __forceinline__ float u01(uint32_t x) {   // (0,1), exact in fp32
@@ -127,29 +139,43 @@ __device__ __forceinline__ void mul_prismatic(Mat34& T, const JointDev& J, float
 // reduction by pi/2 in fp64 (exact for |q| << 2^20), then minimax polynomials
 // in fp32 on [-pi/4, pi/4] (Cephes sinf/cosf): ~25 VALU ops, <= 2 ulp, no
 // large-argument path (ocml sincosf is ~130 ops with a Payne-Hanek branch).
-__device__ __forceinline__ void sincos_joint(double q, float& s, float& c) {
-    const double n = rint(q * 0.63661977236758134308);
-    double r = fma(-n, 1.5707963267948966192, q);
-    r = fma(-n, 6.123233995736766036e-17, r);
-    const float x = (float)r, x2 = x * x;
+__device__ __forceinline__ void sincos_poly(float x, int qd, float& s, float& c) {
+    const float x2 = x * x;
     float sp = fmaf(x2, -1.9515295891e-4f, 8.3321608736e-3f);
     sp = fmaf(x2, sp, -1.6666654611e-1f);
     const float sn = fmaf(x * x2, sp, x);
     float cp = fmaf(x2, 2.443315711809948e-5f, -1.388731625493765e-3f);
     cp = fmaf(x2, cp, 4.166664568298827e-2f);
     const float cs = fmaf(x2 * x2, cp, fmaf(-0.5f, x2, 1.0f));
-    const int qd = (int)n & 3;
+    qd &= 3;
     s = (qd & 1) ? cs : sn;
     c = (qd & 1) ? sn : cs;
     if (qd & 2) s = -s;
     if ((qd + 1) & 2) c = -c;
 }
 
+__device__ __forceinline__ void sincos_joint(double q, float& s, float& c) {
+    const double n = rint(q * 0.63661977236758134308);
+    double r = fma(-n, 1.5707963267948966192, q);
+    r = fma(-n, 6.123233995736766036e-17, r);
+    sincos_poly((float)r, (int)n, s, c);
+}
+
+// fp32 state (torch.sin of a float32 tensor): the same polynomials after a
+// two-constant fp32 Cody-Waite reduction (pi/2 = PIO2_HI + PIO2_MID; the
+// dropped tail is 1.8e-15 * n), no fp64 work.
+__device__ __forceinline__ void sincos_joint(float q, float& s, float& c) {
+    const float n = __builtin_rintf(q * 0.636619772367581343f);
+    float r = fmaf(-n, 1.5707963705062866f, q);
+    r = fmaf(-n, -4.371138828673793e-08f, r);
+    sincos_poly(r, (int)n, s, c);
+}
+
 // One Kinova joint: T <- T * [P | o] * Rz(q), P a signed permutation fixed at
 // compile time (kKinova, mppi_dev.h): the rotation part is register renaming and
 // negation (source modifiers), the translation only its nonzero components.
-template <int J>
-__device__ __forceinline__ void kin_joint(Mat34& T, const float* O, double q) {
+template <int J, typename QT>
+__device__ __forceinline__ void kin_joint(Mat34& T, const float* O, QT q) {
     constexpr KinOrigin k = kKinova[J];
     Mat34 r;
 #pragma unroll
@@ -585,6 +611,10 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                     traj_store(tdst + 2 * plane, posf[c][2]);
                 }
             } else {
+                // joint angle j in the state dtype (fp64 state -> fp64 sin/cos reduction)
+                auto qang = [&](int cc_, int j) {
+                    if constexpr (F64) return posd[cc_][QOFF + j]; else return posf[cc_][QOFF + j];
+                };
                 Mat34 T;   // base (times the folded leading fixed joints)
 #pragma unroll
                 for (int i = 0; i < 12; ++i) T.m[i] = vc.base[i];
@@ -592,20 +622,20 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                     T.m[3] += posf[c][0]; T.m[7] += posf[c][1]; T.m[11] += posf[c][2];
                 }
                 if (NQ == 7 && p.chain_fast == 2) {   // Kinova: origin rotations are signed permutations
-                    kin_joint<0>(T, jnt[p.j0 + 0].O, F64 ? posd[c][QOFF + 0] : (double)posf[c][QOFF + 0]);
-                    kin_joint<1>(T, jnt[p.j0 + 1].O, F64 ? posd[c][QOFF + 1] : (double)posf[c][QOFF + 1]);
-                    kin_joint<2>(T, jnt[p.j0 + 2].O, F64 ? posd[c][QOFF + 2] : (double)posf[c][QOFF + 2]);
-                    kin_joint<3>(T, jnt[p.j0 + 3].O, F64 ? posd[c][QOFF + 3] : (double)posf[c][QOFF + 3]);
-                    kin_joint<4>(T, jnt[p.j0 + 4].O, F64 ? posd[c][QOFF + 4] : (double)posf[c][QOFF + 4]);
-                    kin_joint<5>(T, jnt[p.j0 + 5].O, F64 ? posd[c][QOFF + 5] : (double)posf[c][QOFF + 5]);
-                    kin_joint<6>(T, jnt[p.j0 + 6].O, F64 ? posd[c][QOFF + 6] : (double)posf[c][QOFF + 6]);
+                    kin_joint<0>(T, jnt[p.j0 + 0].O, qang(c, 0));
+                    kin_joint<1>(T, jnt[p.j0 + 1].O, qang(c, 1));
+                    kin_joint<2>(T, jnt[p.j0 + 2].O, qang(c, 2));
+                    kin_joint<3>(T, jnt[p.j0 + 3].O, qang(c, 3));
+                    kin_joint<4>(T, jnt[p.j0 + 4].O, qang(c, 4));
+                    kin_joint<5>(T, jnt[p.j0 + 5].O, qang(c, 5));
+                    kin_joint<6>(T, jnt[p.j0 + 6].O, qang(c, 6));
                 } else if (p.chain_fast) {   // nq revolute-z joints, q_index = 0..nq-1 in order
 #pragma unroll
                     for (int j = 0; j < NQ; ++j) {
                         const JointDev& J = jnt[p.j0 + j];
                         mul_affine(T, J.O);
                         float s, cc;
-                        sincos_joint(F64 ? posd[c][QOFF + j] : (double)posf[c][QOFF + j], s, cc);
+                        sincos_joint(qang(c, j), s, cc);
                         const float omc = 1.0f - cc, r22 = cc + omc;
 #pragma unroll
                         for (int i = 0; i < 3; ++i) {
@@ -630,14 +660,18 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                             }
                         if (J.type == MPPI_JOINT_REVOLUTE) {
                             float s, cc;
-                            sincos_joint(F64 ? qd : (double)qf, s, cc);
+                            if constexpr (F64) sincos_joint(qd, s, cc); else sincos_joint(qf, s, cc);
                             mul_revolute(T, J, cc, s);
                         } else {
                             mul_prismatic(T, J, qf);
                         }
                     }
                 }
-                x = term ? pose_cost(T, vc, p.w_tp, p.w_to) : pose_cost(T, vc, p.w_sp, p.w_so);
+                // the four weights as SGPR values: selecting between two kernel-argument
+                // addresses per lane would otherwise become two vector loads in the FK
+                const float wsp = uniform_f32(p.w_sp), wso = uniform_f32(p.w_so), wtp = uniform_f32(p.w_tp),
+                            wto = uniform_f32(p.w_to);
+                x = pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
                 if (p.store_traj && val) {
 #pragma unroll
                     for (int a = 0; a < NA; ++a) traj_store(tdst + a * plane, posf[c][a]);

@@ -11,6 +11,16 @@ finalize: rho = min_g rho_g, rescale by exp(-(rho_g - rho)/lambda), SavGol,
 u += w_eps.  The payload is (4 + A*H) floats per vehicle per rank -- 2.6 KB at
 H=64, A=10 -- so the collective is latency-bound; ring bandwidth is irrelevant.
 
+Two ways to run the collective:
+
+* ``native=True`` (default when the process group is RCCL, backend "nccl"): the
+  engine owns an RCCL communicator (``mppi_comm_init``; rank 0's unique id is
+  broadcast over torch.distributed) and a whole control step -- rollout, pack,
+  all-reduce, finalize -- is enqueued from C with no Python in between
+  (``Engine.run_steps`` / ``Engine.step`` work unchanged on a shard);
+* ``native=False``: the engine packs into a torch buffer and ``torch.distributed``
+  does the all-reduce (any backend; the gloo tests on CPU and rehearsals use it).
+
 The reference has no distributed code (single process, ``CUDA_VISIBLE_DEVICES='0'``
 at ``mppi.py:31``); there is no reference collective to mirror.
 """
@@ -49,10 +59,14 @@ def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
 class ShardedEngine:
     """One rank's engine of a sample-sharded MPPI controller."""
 
-    def __init__(self, group=None, exchange: Callable = all_reduce_slots, **engine_kw):
+    def __init__(self, group=None, exchange: Callable = all_reduce_slots, native: Optional[bool] = None,
+                 **engine_kw):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if native is None:
+            native = self.world > 1 and dist.get_backend(group) == "nccl" and exchange is all_reduce_slots
+        self.native = bool(native)
         self.local = int(os.environ.get("LOCAL_RANK", engine_kw.pop("device", 0)))
         self.local %= max(1, torch.cuda.device_count())   # more ranks than devices: wrap
         torch.cuda.set_device(self.local)
@@ -64,7 +78,12 @@ class ShardedEngine:
         self.engine.set_stream(self.stream.cuda_stream)
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
-        if self.world > 1:
+        if self.native:   # engine-owned RCCL communicator: the whole step is enqueued from C
+            uid = [Engine.comm_unique_id() if self.rank == 0 else None]
+            if self.world > 1:
+                dist.broadcast_object_list(uid, src=0, group=group)
+            self.engine.comm_init(uid[0])
+        elif self.world > 1:
             slot = self.engine.exchange_slot_floats()
             with torch.cuda.stream(self.stream):
                 self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")
@@ -73,11 +92,24 @@ class ShardedEngine:
 
     def step_async(self, d_noise_ptr: int = 0):
         """rollout -> (all-reduce) -> finalize, all ordered on self.stream, no host sync."""
+        if self.native:
+            self.engine.rollout(d_noise_ptr)
+            self.engine.exchange()
+            self.engine.finalize()
+            return
         with torch.cuda.stream(self.stream):
             self.engine.rollout(d_noise_ptr)
             if self.world > 1:
                 self._exchange(self.buf, self.group)
             self.engine.finalize()
+
+    def run_steps(self, n: int):
+        """n back-to-back control steps; on a native shard one C call enqueues them all."""
+        if self.native or self.world == 1:
+            self.engine.run_steps(n)
+        else:
+            for _ in range(n):
+                self.step_async()
 
     def step(self, state, d_noise_ptr: int = 0):
         self.engine.set_state(state)

@@ -156,6 +156,24 @@ class Engine:
         except Exception:
             pass
 
+    # ------------------------------------------------------- native collective
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """A fresh RCCL unique id (rank 0 makes it; the caller broadcasts it)."""
+        buf = (C.c_uint8 * capi.COMM_ID_BYTES)()
+        capi.check(capi.lib().mppi_comm_unique_id(buf), "comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes):
+        """Join the shard communicator (collective over cfg.shard_count ranks)."""
+        if len(uid) != capi.COMM_ID_BYTES:
+            raise ValueError("comm id must be %d bytes" % capi.COMM_ID_BYTES)
+        buf = (C.c_uint8 * capi.COMM_ID_BYTES).from_buffer_copy(uid)
+        capi.check(self._L.mppi_comm_init(self._h, buf), "comm_init")
+
+    def exchange(self):
+        capi.check(self._L.mppi_exchange(self._h), "exchange")
+
     def set_stream(self, stream_handle: int):
         capi.check(self._L.mppi_set_stream(self._h, C.c_void_p(stream_handle)), "set_stream")
 

@@ -290,6 +290,30 @@ def test_shards_combine_like_one_engine():
     _close(shards[0].get_u_prev(), full.get_u_prev(), rtol=1e-4, atol=1e-6, what="u_prev")
 
 
+def test_native_comm_one_rank_matches_plain_engine():
+    """Engine-owned RCCL communicator (mppi_comm_init) with one rank: every step runs
+    pack -> ncclAllReduce -> combine-from-slots, and must equal the plain engine
+    (the slot combine of one record is the block combine of the same partials)."""
+    K, H = 2048, 32
+    state = np.array([0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 7, np.float64)
+    tgt = ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    plain = _engine(model="arm", n_samples=K, n_horizon=H, seed=11)
+    nat = _engine(model="arm", n_samples=K, n_horizon=H, seed=11)
+    nat.comm_init(nat.comm_unique_id())
+    for e in (plain, nat):
+        e.set_target(*tgt)
+    o1, u1, s1 = plain.step(state)
+    o2, u2, s2 = nat.step(state)
+    _close(u2, u1, rtol=1e-5, atol=1e-7, what="u0 native comm vs plain")
+    _close(o2, o1, rtol=1e-6, atol=1e-9, what="qdes/vdes native comm vs plain")
+    for e in (plain, nat):
+        e.run_steps(5)
+        e.synchronize()
+    _close(nat.get_u_prev(), plain.get_u_prev(), rtol=1e-4, atol=1e-6, what="u_prev after run_steps")
+    nat.close()
+    plain.close()
+
+
 def test_vehicle_batch_equals_single_vehicles():
     """V=4 vehicles in one launch == 4 single-vehicle engines (config C5 path)."""
     K, H = 1024, 64
