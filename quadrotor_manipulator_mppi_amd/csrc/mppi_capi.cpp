@@ -638,7 +638,14 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     const int nw = e->threads / 64;
     const int groups = (e->K + nw * R - 1) / (nw * R);
     int nb = c.blocks_per_vehicle;
-    if (nb <= 0) nb = std::max(1, std::min(groups, (1024 + e->V - 1) / e->V));
+    // auto: one block per group while the grid is at most 512 blocks (2 per CU at 4 waves
+    // per SIMD); above that >= 2 groups per block (the prologue and the block combine are
+    // amortised, fewer records for the finalize), capped at 1024 blocks in total.
+    // Measured on MI355X (tools/geom_sweep.py, profiles/r01/geom_sweep_s3.txt): WB K=8192
+    // 20.2 us at 512 blocks vs 21.6 at 1024; K=65536 best at 1024; V=8 fleet at 128/vehicle.
+    if (nb <= 0) {
+        nb = (groups * e->V <= 512) ? groups : std::min(std::max(1, groups / 2), std::max(1, 1024 / e->V));
+    }
     nb = std::min(nb, groups);
     const int iters = (groups + nb - 1) / nb;
     nb = (groups + iters - 1) / iters;
@@ -1026,6 +1033,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     f.mode = 0;
     f.seq = e->step_ctr + 1u;   // never 0 (the flags start zeroed) unless the counter wraps
     if (f.seq == 0u) f.seq = 1u;
+    if (!record_out) f.seq = 0u;   // no completion flag (and no fence) for unread steps
     if (sharded(e)) {   // slots [shard][v][P]: header then N[a][t]
         const int64_t P = e->dp.P;
         f.nrec = e->cfg.shard_count;
@@ -1189,6 +1197,7 @@ mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, do
     p.step_ctr = e->step_ctr;
     FinParams f = e->fp;
     f.mode = 0;
+    f.seq = 0u;   // the throughput path's finalize (no completion flag)
     block_records(e, f);
     float ms0 = 0.0f, ms1 = 0.0f;
     int rc = 0;

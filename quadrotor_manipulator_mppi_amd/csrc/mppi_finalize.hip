@@ -260,9 +260,13 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
             st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
             st[3] = nanf;
         }
-        // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs)
-        __threadfence_system();
-        __hip_atomic_store(p.flags + (size_t)v * A + a, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs).
+        // seq == 0: nobody waits on this step (mppi_run_steps before its last step) -- no
+        // system-scope fence, whose L2 writeback costs ~1.5 us of kernel time
+        if (p.seq != 0u) {
+            __threadfence_system();
+            __hip_atomic_store(p.flags + (size_t)v * A + a, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     FSTAMP(6);
 }
