@@ -45,6 +45,9 @@ WORKLOADS = {
     "wholebody_c4": dict(model="wholebody", n_samples=8192, n_horizon=64,
                          desc="Whole-body MPPI, 8192 samples/GPU H=64 (BASELINE configs[3] shard)"),
     # configs[4] per-GPU share: 64 vehicles x K=8192 over 8 GPUs -> 8 vehicles per GPU
+    # the 6-DoF rigid-body quadrotor (commented out in the reference), drone sizes
+    "quadrotor_c2": dict(model="quadrotor", n_samples=4096, n_horizon=32,
+                         desc="6-DoF quadrotor MPPI K=4096 H=32 (SURVEY §8f rank 3; configs[1] sizes)"),
     "fleet_c5": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=8,
                      desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
 }
@@ -60,6 +63,8 @@ def make_state(model: str, V: int) -> np.ndarray:
     for v in range(V):
         if model == "drone":
             rows.append([0.0, 0.0, 1.0, 0.0, 0.0, 0.0])
+        elif model == "quadrotor":
+            rows.append([0.0, 0.0, 1.0, 0.0, 0.0, 0.0] + [0.0] * 6)
         elif model == "arm":
             rows.append([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0] + HOME_Q + [0.0] * 7)
         else:
@@ -73,7 +78,7 @@ def make_state(model: str, V: int) -> np.ndarray:
 def set_targets(eng, model, V):
     rng = np.random.default_rng(1)
     for v in range(V):
-        if model == "drone":
+        if model in ("drone", "quadrotor"):
             eng.set_target(DRONE_TARGET, vehicle=v)
         else:
             p = np.array(ARM_TARGET[0]) + (rng.uniform(-0.1, 0.1, 3) if v else 0.0)
@@ -102,7 +107,14 @@ def cpu_baseline(workload: str, budget_s: float):
     K, H, model = w["n_samples"], w["n_horizon"], w["model"]
     threads = torch.get_num_threads()
     times = []
-    if model == "drone":
+    if model == "quadrotor":
+        sig = torch.diag(torch.tensor([30.0, 1.0, 1.0, 1.0]))
+        u = torch.zeros(H, 4)
+        u[:, 0] = 14.7 * 9.81
+
+        def one():
+            return O.quad_step([0, 0, 1.0, 0, 0, 0], [0.0] * 6, u, O.draw_noise(K, H, sig), DRONE_TARGET)
+    elif model == "drone":
         sig = torch.eye(3) * 30.0
         u = torch.zeros(H, 3)
 
@@ -149,6 +161,10 @@ def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=Tru
     se = ShardedEngine(seed=1234, native=native, **w)
     eng = se.engine
     set_targets(eng, w["model"], V)
+    if w["model"] == "quadrotor":   # warm start at hover thrust (quadrotor_mppi.MPPI does the same)
+        u = np.zeros((V, eng.H, eng.A), np.float32)
+        u[..., 0] = eng.cfg.quad_mass * eng.cfg.quad_gravity
+        eng.set_u_prev(u)
     state = make_state(w["model"], V)
     eng.set_state(state)
 
@@ -213,7 +229,7 @@ def main():
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", default="drone_c2,wholebody_c4",
+    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
 

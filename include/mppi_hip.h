@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 3
+#define MPPI_ABI_VERSION 4
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
@@ -61,7 +61,10 @@ typedef enum {
 typedef enum {
     MPPI_MODEL_DRONE = 0,     /* xyz double integrator, squared position cost      (A=3)  drone_mppi.py   */
     MPPI_MODEL_ARM = 1,       /* joint double integrator + FK chain + pose cost    (A=nq) mppi.py         */
-    MPPI_MODEL_WHOLEBODY = 2  /* drone xyz + arm joints, mobile-base FK, pose cost (A=3+nq) SURVEY A16    */
+    MPPI_MODEL_WHOLEBODY = 2, /* drone xyz + arm joints, mobile-base FK, pose cost (A=3+nq) SURVEY A16    */
+    MPPI_MODEL_QUADROTOR = 3  /* 6-DoF rigid-body quadrotor: thrust + body torques, Euler-angle attitude,
+                               * squared position cost (A=4, H <= 64).  The model the reference ships
+                               * commented out (drone_mppi.py:57-83, drone.py:114-154) */
 } mppi_model;
 
 typedef enum {
@@ -125,6 +128,12 @@ typedef struct {
     float q_center[MPPI_MAX_JOINTS];   /* centering target per arm joint                         */
     float q_lower[MPPI_MAX_JOINTS];    /* joint limits                                           */
     float q_upper[MPPI_MAX_JOINTS];
+    /* MPPI_MODEL_QUADROTOR rigid body (drone.urdf:15-16; g and kd are undefined in the
+     * commented reference loop, drone_mppi.py:64-79): */
+    float quad_mass;            /* 14.7 kg                                                      */
+    float quad_inertia[3];      /* diagonal body inertia 1.57, 3.93, 2.59                       */
+    float quad_kd;              /* linear drag coefficient kd (0)                               */
+    float quad_gravity;         /* g = (0, 0, -quad_gravity), 9.81                              */
 } mppi_config;
 
 typedef enum {
@@ -183,6 +192,8 @@ mppi_status mppi_get_u_prev(mppi_engine* e, float* u_prev);
  *   DRONE:     x(3) v(3)
  *   ARM:       base xyz(3) quat xyzw(4) q(nq) qd(nq)        (q_full[:7]+q_full[7:], v_full[6:])
  *   WHOLEBODY: base xyz(3) quat xyzw(4) q(nq) base vel(3) qd(nq)
+ *   QUADROTOR: xyz(3) rpy(3) (roll, pitch, yaw; R = Rz(yaw) Ry(pitch) Rx(roll), drone.py:126-154)
+ *              v world(3) omega body(3)
  * Async host->device (pinned staging) on the engine stream. */
 mppi_status mppi_set_state(mppi_engine* e, const double* state);
 
@@ -215,6 +226,7 @@ mppi_status mppi_exchange(mppi_engine* e);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles
  *   DRONE: x_des(3) v_des(3);  ARM: qdes(nq) vdes(nq);  WHOLEBODY: x(3) v(3) qdes(nq) vdes(nq)
+ *   QUADROTOR: x_des = (xyz, rpy)(6), v_des = (v, omega)(6): the model's first step under u0
  * u0 (V, A) floats and stats (V) may be NULL. */
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats);
 
@@ -237,6 +249,7 @@ mppi_status mppi_synchronize(mppi_engine* e);
  *   weights  w (V,K)                         compute_weights()
  *   noise    eps (V,K,H,A)                   sampling()            [store_noise]
  *   traj     (V,K,H,C) C = traj_channels    DRONE p(3) / ARM q(nq)+EE(16) / WB p(3)+q(nq)+EE(16)
+ *                                            QUADROTOR xyz(3)+rpy(3) (drone_mppi.py:62 trajectory)
  *            EE as the 4x4 row-major matrix of urdf_fk.py:108       [store_trajectory]
  *   wnoise   w_eps before / after SavGol (V,H,A)                     */
 mppi_status mppi_get_costs(mppi_engine* e, float* S);

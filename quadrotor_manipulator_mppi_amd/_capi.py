@@ -16,12 +16,12 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPPI_HIP_LIB", os.path.join(PKG, "lib", "libmppi_hip.so"))
 
 MAX_ACTION, MAX_JOINTS, MAX_HORIZON, MAX_SAVGOL = 16, 16, 256, 31
-MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY = 0, 1, 2
+MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY, MODEL_QUADROTOR = 0, 1, 2, 3
 NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC = 0, 1, 2
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 3
+ABI_VERSION = 4
 COMM_ID_BYTES = 128
 
 
@@ -48,7 +48,9 @@ class Config(C.Structure):
                 ("cost_gamma", C.c_float), ("w_center", C.c_float), ("w_joint_track", C.c_float),
                 ("w_action", C.c_float), ("joint_limit_penalty", C.c_float),
                 ("q_center", C.c_float * MAX_JOINTS), ("q_lower", C.c_float * MAX_JOINTS),
-                ("q_upper", C.c_float * MAX_JOINTS)]
+                ("q_upper", C.c_float * MAX_JOINTS),
+                ("quad_mass", C.c_float), ("quad_inertia", C.c_float * 3), ("quad_kd", C.c_float),
+                ("quad_gravity", C.c_float)]
 
 
 class Stats(C.Structure):

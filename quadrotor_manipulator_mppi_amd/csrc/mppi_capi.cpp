@@ -376,6 +376,11 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
                 vc.pos0f[a] = (float)s[a]; vc.vel0f[a] = (float)s[3 + a];
                 vc.pos0[a] = vc.pos0f[a]; vc.vel0[a] = vc.vel0f[a];
             }
+        } else if (c.model == MPPI_MODEL_QUADROTOR) {   // xyz rpy | v omega (float32 tensors)
+            for (int a = 0; a < 6; ++a) {
+                vc.pos0f[a] = (float)s[a]; vc.vel0f[a] = (float)s[6 + a];
+                vc.pos0[a] = vc.pos0f[a]; vc.vel0[a] = vc.vel0f[a];
+            }
         } else if (c.model == MPPI_MODEL_ARM) {
             float T16[16];
             if (c.state_f64) base_from_xyzquat_t<double>(s, T16);
@@ -405,6 +410,33 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
         }
     }
     return MPPI_OK;
+}
+
+// QUADROTOR outputs: the model's first step (k_rollout_quad, t = 0) under the new u[0],
+// in fp32 as the device / the reference's float32 tensors: x_des = (p, rpy) and
+// v_des = (v, omega) after one step (the drone returns the same pair, drone_mppi.py:168-175).
+void quad_outputs(const mppi_engine* e, const double* s, const float* u0, double* out) {
+    const DevParams& p = e->dp;
+    const float dt = p.dt;
+    float x[12];
+    for (int i = 0; i < 12; ++i) x[i] = (float)s[i];
+    const float sr = std::sin(x[3]), cr = std::cos(x[3]), sp = std::sin(x[4]), cp = std::cos(x[4]);
+    const float sy = std::sin(x[5]), cy = std::cos(x[5]);
+    const float tp = sp / cp;
+    const float r02 = cy * sp * cr + sy * sr, r12 = sy * sp * cr - cy * sr, r22 = cp * cr;
+    const float wx = x[9], wy = x[10], wz = x[11];
+    const float dr = wx + sr * tp * wy + cr * tp * wz;
+    const float dpi = cr * wy - sr * wz;
+    const float dya = sr / cp * wy + cr / cp * wz;
+    out[0] = x[0] + dt * x[6]; out[1] = x[1] + dt * x[7]; out[2] = x[2] + dt * x[8];
+    out[3] = x[3] + dt * dr; out[4] = x[4] + dt * dpi; out[5] = x[5] + dt * dya;
+    const float thr = u0[0];
+    out[6] = x[6] + dt * (p.q_inv_m * (r02 * thr - p.q_kd * x[6]));
+    out[7] = x[7] + dt * (p.q_inv_m * (r12 * thr - p.q_kd * x[7]));
+    out[8] = x[8] + dt * (-p.q_g + p.q_inv_m * (r22 * thr - p.q_kd * x[8]));
+    out[9] = wx + dt * (p.q_iinv[0] * u0[1]);
+    out[10] = wy + dt * (p.q_iinv[1] * u0[2]);
+    out[11] = wz + dt * (p.q_iinv[2] * u0[3]);
 }
 
 mppi_status upload_consts(mppi_engine* e) {
@@ -449,7 +481,7 @@ mppi_status drain_timing(mppi_engine* e) {
 }
 
 mppi_status validate(const mppi_config& c) {
-    if (c.model < 0 || c.model > 2) return fail(MPPI_ERR_INVALID_ARG, "unknown model %d", c.model);
+    if (c.model < 0 || c.model > 3) return fail(MPPI_ERR_INVALID_ARG, "unknown model %d", c.model);
     if (c.n_vehicles < 1 || c.n_samples < 1 || c.n_horizon < 2 || c.n_horizon > MPPI_MAX_HORIZON)
         return fail(MPPI_ERR_INVALID_ARG, "bad sizes V=%d K=%d H=%d", c.n_vehicles, c.n_samples, c.n_horizon);
     if (c.model == MPPI_MODEL_DRONE && c.n_action != 3)
@@ -460,7 +492,14 @@ mppi_status validate(const mppi_config& c) {
     if (c.model == MPPI_MODEL_WHOLEBODY && c.n_action != 10)
         return fail(MPPI_ERR_INVALID_ARG, "WHOLEBODY kernels are built for 3 + 7 dims (n_action 10, got %d)",
                     c.n_action);
-    if (c.model != MPPI_MODEL_DRONE) {
+    if (c.model == MPPI_MODEL_QUADROTOR) {
+        if (c.n_action != 4) return fail(MPPI_ERR_INVALID_ARG, "QUADROTOR needs n_action=4 (thrust + 3 torques)");
+        if (c.n_horizon > 64) return fail(MPPI_ERR_INVALID_ARG, "QUADROTOR supports H <= 64 (got %d)", c.n_horizon);
+        if (!(c.quad_mass > 0.0f) || !(c.quad_inertia[0] > 0.0f) || !(c.quad_inertia[1] > 0.0f) ||
+            !(c.quad_inertia[2] > 0.0f))
+            return fail(MPPI_ERR_INVALID_ARG, "QUADROTOR needs a positive mass and inertia");
+    }
+    if (c.model == MPPI_MODEL_ARM || c.model == MPPI_MODEL_WHOLEBODY) {
         if (c.n_joints < 1 || c.n_joints > MPPI_MAX_JOINTS)
             return fail(MPPI_ERR_INVALID_ARG, "n_joints=%d", c.n_joints);
         const int nq = nq_of(c);
@@ -482,7 +521,7 @@ mppi_status validate(const mppi_config& c) {
     if (c.shard_count < 1 || c.shard_rank < 0 || c.shard_rank >= c.shard_count)
         return fail(MPPI_ERR_INVALID_ARG, "shard %d/%d", c.shard_rank, c.shard_count);
     if (c.cost_terms & ~0x1F) return fail(MPPI_ERR_INVALID_ARG, "unknown cost_terms bits 0x%x", c.cost_terms);
-    if (c.cost_terms && c.model == MPPI_MODEL_DRONE)
+    if (c.cost_terms && (c.model == MPPI_MODEL_DRONE || c.model == MPPI_MODEL_QUADROTOR))
         return fail(MPPI_ERR_INVALID_ARG, "cost_terms apply to the ARM / WHOLEBODY CostManager (not DRONE)");
     if (c.block_threads && (c.block_threads % 64 || c.block_threads > 512))
         return fail(MPPI_ERR_INVALID_ARG, "block_threads must be a multiple of 64 <= 512");
@@ -520,6 +559,12 @@ void mppi_config_default(mppi_config* c, int32_t model) {
         for (int a = 0; a < 3; ++a) c->sigma[a * 3 + a] = 30.0f;
         c->w_stage_pos = 100.0f; c->w_term_pos = 20.0f;
         c->savgol_window = 5;
+    } else if (model == MPPI_MODEL_QUADROTOR) {  // the drone controller's sizes and cost (drone_mppi.py:16-35,
+        c->n_samples = 1000; c->n_action = 4;     // 87-107, 160); Sigma is build-defined: 30 N on the thrust
+        c->sigma[0] = 30.0f;                      // (the drone's 30), 1 N m on each torque
+        for (int a = 1; a < 4; ++a) c->sigma[a * 4 + a] = 1.0f;
+        c->w_stage_pos = 100.0f; c->w_term_pos = 20.0f;
+        c->savgol_window = 5;
     } else {                                     // mppi.py:37-75; cost_manager.py:25-28
         c->n_samples = 100;
         c->n_action = (model == MPPI_MODEL_ARM) ? 7 : 10;
@@ -547,11 +592,16 @@ void mppi_config_default(mppi_config* c, int32_t model) {
         c->q_lower[j] = j < 7 ? lo[j] : -INFINITY;
         c->q_upper[j] = j < 7 ? hi[j] : INFINITY;
     }
+    c->quad_mass = 14.7f;                                  // drone.urdf:15-16
+    c->quad_inertia[0] = 1.57f; c->quad_inertia[1] = 3.93f; c->quad_inertia[2] = 2.59f;
+    c->quad_kd = 0.0f;
+    c->quad_gravity = 9.81f;
 }
 
 int32_t mppi_state_dim(const mppi_config* c) {
     const int nq = nq_of(*c);
     if (c->model == MPPI_MODEL_DRONE) return 6;
+    if (c->model == MPPI_MODEL_QUADROTOR) return 12;
     if (c->model == MPPI_MODEL_ARM) return 7 + 2 * nq;
     return 7 + nq + 3 + nq;
 }
@@ -559,12 +609,14 @@ int32_t mppi_state_dim(const mppi_config* c) {
 int32_t mppi_output_dim(const mppi_config* c) {
     const int nq = nq_of(*c);
     if (c->model == MPPI_MODEL_DRONE) return 6;
+    if (c->model == MPPI_MODEL_QUADROTOR) return 12;
     if (c->model == MPPI_MODEL_ARM) return 2 * nq;
     return 6 + 2 * nq;
 }
 
 int32_t mppi_traj_channels(const mppi_config* c) {
     if (c->model == MPPI_MODEL_DRONE) return 3;
+    if (c->model == MPPI_MODEL_QUADROTOR) return 6;
     return c->n_action + 16;
 }
 
@@ -572,7 +624,7 @@ int64_t mppi_rollout_bytes(const mppi_config* c) {
     // algorithmic bytes of one rollout launch: trajectory planes written
     // (+ injected eps read, + eps written when stored) + S + partial records
     const int64_t KH = (int64_t)c->n_vehicles * c->n_samples * c->n_horizon;
-    const int64_t C = (c->model == MPPI_MODEL_DRONE) ? 3 : c->n_action + 12;
+    const int64_t C = (c->model == MPPI_MODEL_DRONE) ? 3 : (c->model == MPPI_MODEL_QUADROTOR) ? 6 : c->n_action + 12;
     int64_t b = 0;
     if (c->store_trajectory) b += KH * C * 4;
     if (c->noise_mode == MPPI_NOISE_INJECTED) b += KH * c->n_action * 4;
@@ -619,7 +671,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     e->qoff = (c.model == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     e->state_dim = mppi_state_dim(&c);
     e->out_dim = mppi_output_dim(&c);
-    e->C = (c.model == MPPI_MODEL_DRONE) ? 3 : e->A + 12;
+    e->C = (c.model == MPPI_MODEL_DRONE) ? 3 : (c.model == MPPI_MODEL_QUADROTOR) ? 6 : e->A + 12;
     e->tpos.assign((size_t)3 * e->V, 0.0f);
     e->tquat.assign((size_t)4 * e->V, 0.0f);
     for (int v = 0; v < e->V; ++v) e->tquat[4 * v + 3] = 1.0f;
@@ -647,8 +699,13 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
         nb = (groups * e->V <= 512) ? groups : std::min(std::max(1, groups / 2), std::max(1, 1024 / e->V));
     }
     nb = std::min(nb, groups);
-    const int iters = (groups + nb - 1) / nb;
+    int iters = (groups + nb - 1) / nb;
     nb = (groups + iters - 1) / iters;
+    if (c.model == MPPI_MODEL_QUADROTOR) {   // k_rollout_quad: one wave of 64 rollouts per block
+        e->threads = 64;
+        nb = (e->K + 63) / 64;
+        iters = 1;
+    }
     if (nb > 4096) { delete e; return fail(MPPI_ERR_INVALID_ARG, "too many rollout blocks (%d)", nb); }
     const int P = (kHdr + e->A * H + 3) & ~3;
 
@@ -788,6 +845,9 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.w_cov = (float)((double)c.w_covar * (c.lambda_ * (1.0 - (double)c.cost_alpha)));   // covar_cost.py:15,24
     p.w_cen = c.w_center; p.w_jt = c.w_joint_track; p.w_act = c.w_action; p.lim_pen = c.joint_limit_penalty;
     p.sinv = e->d_sinv; p.gamma_t = e->d_gamma; p.jtraj = e->d_jtraj;
+    p.q_inv_m = (float)(1.0 / (double)c.quad_mass);   // 1/self.m as a Python float, used in fp32
+    for (int d = 0; d < 3; ++d) p.q_iinv[d] = (float)(1.0 / (double)c.quad_inertia[d]);
+    p.q_kd = c.quad_kd; p.q_g = c.quad_gravity;
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS
@@ -1119,6 +1179,9 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
     const float* uu = (const float*)(e->h_out + off_u0(e));
     const float* st = (const float*)(e->h_out + off_stats(e));
     if (out) std::memcpy(out, o, sizeof(double) * e->V * e->out_dim);
+    if (out && e->cfg.model == MPPI_MODEL_QUADROTOR)
+        for (int v = 0; v < e->V; ++v)
+            quad_outputs(e, e->state.data() + (size_t)v * e->state_dim, uu + (size_t)v * e->A, out + (size_t)v * e->out_dim);
     if (u0) std::memcpy(u0, uu, sizeof(float) * e->V * e->A);
     bool nonfinite = false;
     for (int v = 0; v < e->V; ++v) {
@@ -1272,13 +1335,16 @@ mppi_status mppi_get_trajectory(mppi_engine* e, float* traj) {
     HIP_TRY(hipMemcpyAsync(soa.data(), e->d_traj, n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     const int Cr = mppi_traj_channels(&e->cfg);
-    const int nstate = (e->cfg.model == MPPI_MODEL_DRONE) ? 3 : e->A;
+    const bool has_ee = e->cfg.model == MPPI_MODEL_ARM || e->cfg.model == MPPI_MODEL_WHOLEBODY;
+    const int nstate = has_ee ? e->A : e->C;
+    const bool t_major = e->cfg.model == MPPI_MODEL_QUADROTOR;   // (V,C,H,K) planes (k_rollout_quad)
     for (int v = 0; v < e->V; ++v)
         for (size_t i = 0; i < KH; ++i) {
             float* dst = traj + ((size_t)v * KH + i) * Cr;
-            const float* src = soa.data() + (size_t)v * e->C * KH + i;
+            const size_t ii = t_major ? (i % e->H) * e->K + i / e->H : i;
+            const float* src = soa.data() + (size_t)v * e->C * KH + ii;
             for (int c = 0; c < nstate; ++c) dst[c] = src[c * KH];
-            if (e->cfg.model != MPPI_MODEL_DRONE) {
+            if (has_ee) {
                 float* ee = dst + nstate;
                 for (int r = 0; r < 12; ++r) ee[r] = src[(nstate + r) * KH];
                 ee[12] = 0.0f; ee[13] = 0.0f; ee[14] = 0.0f; ee[15] = 1.0f;

@@ -107,6 +107,11 @@ struct DevParams {
     const float* sinv;            // (A,A) Sigma^-1, fp32
     const float* gamma_t;         // (H) fp32 gamma^t
     const float* jtraj;           // (V,H,nq) joint tracking target
+    // QUADROTOR rigid body (mppi_config.quad_*): fp32 as the reference's tensors
+    float q_inv_m;                // fp32(1 / mass) (the Python-float 1/self.m of drone_mppi.py:68)
+    float q_iinv[3];              // fp32(1 / I_ii), diagonal inertia
+    float q_kd;                   // linear drag
+    float q_g;                    // gravity magnitude, g = (0, 0, -q_g)
 };
 constexpr int kStamps = 16;
 
@@ -151,6 +156,7 @@ int mppi_launch_rollout(const mppi::DevParams* p, int block_threads, void* strea
 int mppi_launch_rollout_arm64(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_arm32(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_wb(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_rollout_quad(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_finalize(const mppi::FinParams* p, void* stream);
 int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int K, float coef,
                         void* stream);

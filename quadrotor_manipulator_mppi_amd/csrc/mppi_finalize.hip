@@ -233,7 +233,10 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restric
         p.u0[(size_t)v * A + a] = u0;
         double* out = p.out + (size_t)v * p.out_dim;
         const bool drone_dim = (p.model == MPPI_MODEL_DRONE) || (p.model == MPPI_MODEL_WHOLEBODY && a < 3);
-        if (drone_dim) {   // drone_mppi.py:168-169
+        if (p.model == MPPI_MODEL_QUADROTOR) {
+            // coupled dims (thrust rotated by R(rpy)): the host forms the outputs from u0
+            // (mppi_capi.cpp quad_outputs)
+        } else if (drone_dim) {   // drone_mppi.py:168-169
             const float x0 = x0f, v0 = v0f;
             const float xo = (x0 + v0 * p.dt) + (0.5f * u0) * p.dt2;
             const float vo = v0 + p.dt * u0;

@@ -34,6 +34,9 @@ extern "C" int mppi_launch_rollout(const DevParams* p, int threads, void* stream
         case MPPI_MODEL_WHOLEBODY:
             if (p->A == 10) return mppi_launch_rollout_wb(p, threads, stream);
             break;
+        case MPPI_MODEL_QUADROTOR:
+            if (p->A == 4) return mppi_launch_rollout_quad(p, threads, stream);
+            break;
     }
     return -1;
 }

@@ -15,7 +15,9 @@ import numpy as np
 from . import _capi as capi
 from .robot.urdf_chain import load_chain
 
-MODELS = {"drone": capi.MODEL_DRONE, "arm": capi.MODEL_ARM, "wholebody": capi.MODEL_WHOLEBODY}
+MODELS = {"drone": capi.MODEL_DRONE, "arm": capi.MODEL_ARM, "wholebody": capi.MODEL_WHOLEBODY,
+          "quadrotor": capi.MODEL_QUADROTOR}
+QUAD_FIELDS = ("quad_mass", "quad_kd", "quad_gravity")
 JOINT_TYPES = {"fixed": capi.JOINT_FIXED, "revolute": capi.JOINT_REVOLUTE,
                "continuous": capi.JOINT_REVOLUTE, "prismatic": capi.JOINT_PRISMATIC}
 
@@ -54,13 +56,14 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
                 seed: int = 0x5EED, device: int = 0, shard_rank: int = 0, shard_count: int = 1,
                 state_f64: Optional[bool] = None, store_trajectory: bool = True, store_noise: bool = False,
                 check_reach: Optional[bool] = None, reach_tol: float = 0.005, blocks_per_vehicle: int = 0,
-                block_threads: int = 0, cost_terms=0, cost_weights: Optional[Dict[str, float]] = None
-                ) -> capi.Config:
+                block_threads: int = 0, cost_terms=0, cost_weights: Optional[Dict[str, float]] = None,
+                quad: Optional[Dict] = None) -> capi.Config:
     """``cost_terms``: bitmask of ``capi.COST_*`` or an iterable of names among
     ``covar, center, joint_track, action, joint_limit`` -- the CostManager terms the
     reference ships disabled (cost_manager.py:83-87).  ``cost_weights`` overrides
     ``w_covar, cost_alpha, cost_gamma, w_center, w_joint_track, w_action,
-    joint_limit_penalty``."""
+    joint_limit_penalty``.  ``quad`` overrides the QUADROTOR rigid body: ``quad_mass``,
+    ``quad_inertia`` (3,), ``quad_kd``, ``quad_gravity``."""
     L = capi.lib()
     cfg = capi.Config()
     L.mppi_config_default(C.byref(cfg), MODELS[model])
@@ -83,8 +86,16 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
             cfg.sigma[i] = float(s.reshape(-1)[i])
     if weights is not None:
         cfg.w_stage_pos, cfg.w_stage_ori, cfg.w_term_pos, cfg.w_term_ori = map(float, weights)
-    if model != "drone":
+    if model in ("arm", "wholebody"):
         fill_joints(cfg, chain if chain is not None else load_chain())
+    for k, val in (quad or {}).items():
+        if k == "quad_inertia":
+            for d in range(3):
+                cfg.quad_inertia[d] = float(val[d])
+        elif k in QUAD_FIELDS:
+            setattr(cfg, k, float(val))
+        else:
+            raise ValueError(f"unknown quadrotor parameter {k!r}")
     if savgol_window is not None:
         cfg.savgol_window = savgol_window
     cfg.savgol_order = savgol_order

@@ -1,0 +1,95 @@
+"""GPU parity of the 6-DoF quadrotor model (k_rollout_quad + k_finalize through the
+C-ABI) against the torch restatement ``oracle.mppi_oracle.quad_step`` on the same
+injected noise.  PARITY UNPINNED with respect to the reference: it ships this model
+only as commented code (drone_mppi.py:57-83), so the oracle is the checker.
+
+Tolerances (sequential fp32 dynamics; the device uses <= 2 ulp polynomial sin/cos and
+sin/cos division for tan where torch calls sinf/cosf/tanf):
+* trajectory xyz / rpy: 5e-5 absolute over H <= 64 steps;
+* S: 1e-4 relative;
+* the reduction given the GPU's own S: 1e-5 relative; end to end within the softmin's
+  conditioning bound (as the arm fixtures);
+* outputs (first model step under u[0]): 1e-5 absolute.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mppi_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIG = np.diag([30.0, 1.0, 1.0, 1.0]).astype(np.float32)
+
+
+def _engine(**kw):
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    return Engine(make_config(model="quadrotor", **kw))
+
+
+def _close(got, want, rtol=0.0, atol=0.0, what=""):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    err = np.abs(got - want)
+    bad = err > atol + rtol * np.abs(want)
+    assert not bad.any(), f"{what}: {bad.sum()}/{bad.size} off, max err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("K,H,seed", [(256, 32, 0), (100, 64, 1), (64, 20, 2)])
+def test_quadrotor_matches_oracle(K, H, seed):
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    x = [0.2, -0.1, 2.5, 0.05, -0.08, 0.7]
+    v = [0.3, -0.2, 0.1, 0.2, -0.1, 0.05]
+    target = [0.5, 0.4, 3.0]
+    u = np.zeros((H, 4), np.float32)
+    u[:, 0] = 14.7 * 9.81
+    u += rng.normal(0, 0.5, (H, 4)).astype(np.float32)
+    e = _engine(n_samples=K, n_horizon=H, noise="injected", sigma=SIG)
+    e.set_target(np.asarray(target, np.float32))
+    for s in range(2):
+        noise = O.draw_noise(K, H, torch.from_numpy(SIG))
+        ref = O.quad_step(x, v, torch.from_numpy(u), noise, target)
+        e.set_u_prev(u)
+        out, u0, st = e.step(np.asarray(x + v, np.float64), noise.numpy()[None])
+        _close(e.get_trajectory()[0], ref["traj"].numpy(), atol=5e-5, what="traj")
+        S, S_ref = e.get_costs()[0], ref["S"].numpy()
+        _close(S, S_ref, rtol=1e-4, what="S")
+        w_own = O.softmin(torch.from_numpy(S), 0.1).numpy()
+        raw, sm = e.get_weighted_noise()
+        _close(raw[0], np.einsum("k,kha->ha", w_own.astype(np.float64), noise.numpy()), rtol=1e-5, atol=1e-6,
+               what="w_eps | S_gpu")
+        dS = float(np.max(np.abs(S.astype(np.float64) - S_ref)))
+        w_ref = ref["w"].numpy().astype(np.float64)
+        bound = (2.0 / 0.1) * dS * np.einsum("k,kha->ha", w_ref, np.abs(noise.numpy())) * 1.5 + 2e-5
+        assert np.all(np.abs(raw[0] - ref["w_eps_raw"].numpy()) <= bound)
+        u_new = e.get_u_prev()[0]
+        _close(u_new, ref["u_prev_out"].numpy(), atol=float(bound.max()) * 4 + 1e-4, what="u_prev")
+        # outputs: the first model step under the device's own u[0]
+        one = O.quad_rollout(torch.from_numpy(u0[0]).view(1, 1, 4), x, v)[0, 0].numpy()
+        _close(out[0, :6], one, atol=1e-5, what="x_des")
+        assert not st[0].nonfinite
+        Iinv = np.array([1 / 1.57, 1 / 3.93, 1 / 2.59])
+        _close(out[0, 9:12], np.asarray(v[3:]) + 0.01 * Iinv * u0[0, 1:], atol=1e-5, what="omega_des")
+        u = u_new
+
+
+def test_quadrotor_device_noise_and_dropin():
+    """Philox mode draws eps = z * diag(Sigma) from the shared counter scheme, and the
+    drop-in class flies toward the target over a few steps."""
+    from quadrotor_manipulator_mppi_amd.engine import philox_normals
+    from quadrotor_manipulator_mppi_amd.mppi_solver.quadrotor_mppi import MPPI
+    K, H = 128, 32
+    e = _engine(n_samples=K, n_horizon=H, sigma=SIG, store_noise=True, seed=77)
+    e.set_target(np.asarray([0, 0, 3.4], np.float32))
+    e.step(np.asarray([0, 0, 3.0, 0, 0, 0] + [0.0] * 6, np.float64))
+    raw, z = philox_normals(77, 0, 0, 0, K, H, 4)
+    _close(e.get_noise()[0], z * np.diag(SIG), rtol=1e-6, atol=1e-6, what="device eps")
+    m = MPPI(n_samples=1024)
+    m.target = [0.0, 0.0, 3.4]
+    x, v = np.array([0, 0, 3.0, 0, 0, 0.0]), np.zeros(6)
+    for _ in range(30):
+        m.set_state(x, v)
+        xd, vd = m.compute_control_input()
+        x, v = xd.cpu().numpy().astype(np.float64), vd.cpu().numpy().astype(np.float64)
+    assert np.isfinite(x).all() and x[2] > 3.0 + 1e-4      # climbing toward z* = 3.4

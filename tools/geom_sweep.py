@@ -10,7 +10,7 @@ NBS = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0]
 THS = [int(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0]
 V = int(os.environ.get("GEOM_V", "1"))
 sd = {"arm": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 7,
-      "drone": [0, 0, 1, 0, 0, 0], "wholebody": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 10}[model]
+      "drone": [0, 0, 1, 0, 0, 0], "quadrotor": [0, 0, 1, 0, 0, 0] + [0.0] * 6, "wholebody": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0] * 10}[model]
 for th in THS:
     for nb in NBS:
         e = Engine(make_config(model, n_samples=K, n_horizon=H, n_vehicles=V, blocks_per_vehicle=nb,
