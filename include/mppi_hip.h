@@ -72,7 +72,12 @@ typedef enum {
     MPPI_NOISE_INJECTED = 1   /* caller supplies eps (K,H,A) per step (parity: reference randn noise)  */
 } mppi_noise_mode;
 
-typedef enum { MPPI_JOINT_FIXED = 0, MPPI_JOINT_REVOLUTE = 1, MPPI_JOINT_PRISMATIC = 2 } mppi_joint_type;
+typedef enum {
+    MPPI_JOINT_FIXED = 0,
+    MPPI_JOINT_REVOLUTE = 1,
+    MPPI_JOINT_PRISMATIC = 2,
+    MPPI_JOINT_FLOATING = 3   /* free-flyer root of the dynamics model only (mppi_link)            */
+} mppi_joint_type;
 
 /* One entry of the active joint chain (urdfparser.py:133-161). xyz/rpy/axis as
  * the URDF floats (rounded to fp32 like torch.tensor(jt.origin.xyz)). */
@@ -286,6 +291,42 @@ mppi_status mppi_host_fk(const mppi_joint* joints, int32_t n_joints, const doubl
  * exactly as the rollout kernel draws them for (seed, step, vehicle, global k0..k0+K). */
 mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, int64_t k0, int32_t K,
                                 int32_t H, int32_t A, int32_t device, float* z, uint32_t* raw);
+
+/* ---------------------------------------------------------------------------------------
+ * Host rigid-body dynamics of the arm node.  The reference node
+ * calls pin.computeAllTerms(model, data, q, v) on the free-flyer model of
+ * full_robot_floating2.urdf every tick (kinova.py:54-61, 126) and applies
+ *     tau = M[6:,6:] (400 (qdes - q[7:]) - 40 v[6:]) + nle[6:]              (kinova.py:184)
+ * These replace those Pinocchio calls (double precision, Pinocchio's conventions: q = base
+ * xyz + quaternion xyzw + joints, v = base linear + angular velocity in the base frame +
+ * joint rates, gravity (0,0,-g)).  Fixed-joint links are merged into their movable
+ * ancestor.  K = 1 per tick: host code, no GPU. */
+typedef struct {
+    int32_t parent;        /* index of the parent link entry, -1 = the world                  */
+    int32_t type;          /* joint attaching this link: MPPI_JOINT_FIXED / REVOLUTE /
+                            * PRISMATIC / FLOATING (root only)                                 */
+    double xyz[3], rpy[3]; /* joint origin in the parent link frame (URDF <origin>)           */
+    double axis[3];        /* joint axis in the joint frame (URDF <axis>)                     */
+    double mass;           /* URDF <inertial>: mass, COM in the link frame, inertia about the */
+    double com[3];         /*   COM in the link frame (row-major 3x3; the <inertial> origin    */
+    double inertia[9];     /*   rotation already applied)                                     */
+} mppi_link;
+
+typedef struct mppi_dyn mppi_dyn;
+
+/* Build the model from links in topological order (robot/urdf_tree.py writes them). */
+mppi_status mppi_dyn_create(const mppi_link* links, int32_t n_links, double gravity, mppi_dyn** out);
+void mppi_dyn_destroy(mppi_dyn* d);
+void mppi_dyn_dims(const mppi_dyn* d, int32_t* nq, int32_t* nv, int32_t* n_bodies);
+/* Inverse dynamics tau = M(q) a + nle(q, v) (a NULL = 0), recursive Newton-Euler. */
+mppi_status mppi_dyn_rnea(mppi_dyn* d, const double* q, const double* v, const double* a, double* tau);
+/* pin.computeAllTerms' M (nv x nv, row-major) and nle = C(q,v) v + g(q) (nv); either may be NULL. */
+mppi_status mppi_dyn_terms(mppi_dyn* d, const double* q, const double* v, double* M, double* nle);
+/* kinova.py:184 for the trailing actuated joints (rows first_v..nv-1):
+ * tau = M[first_v:, first_v:] (kp (qdes - q_act) - kd v_act) + nle[first_v:], as ONE RNEA
+ * pass with a = (0, ades) (the base-acceleration columns of M are multiplied by 0). */
+mppi_status mppi_computed_torque(mppi_dyn* d, const double* q, const double* v, const double* qdes, double kp,
+                                 double kd, int32_t first_v, double* tau);
 
 #ifdef __cplusplus
 }

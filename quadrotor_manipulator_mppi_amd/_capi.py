@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MPPI_HIP_LIB", os.path.join(PKG, "lib", "libmppi_hip.
 MAX_ACTION, MAX_JOINTS, MAX_HORIZON, MAX_SAVGOL = 16, 16, 256, 31
 MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY, MODEL_QUADROTOR = 0, 1, 2, 3
 NOISE_PHILOX, NOISE_INJECTED = 0, 1
-JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC = 0, 1, 2
+JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
 ABI_VERSION = 4
@@ -51,6 +51,12 @@ class Config(C.Structure):
                 ("q_upper", C.c_float * MAX_JOINTS),
                 ("quad_mass", C.c_float), ("quad_inertia", C.c_float * 3), ("quad_kd", C.c_float),
                 ("quad_gravity", C.c_float)]
+
+
+class Link(C.Structure):
+    _fields_ = [("parent", C.c_int32), ("type", C.c_int32), ("xyz", C.c_double * 3), ("rpy", C.c_double * 3),
+                ("axis", C.c_double * 3), ("mass", C.c_double), ("com", C.c_double * 3),
+                ("inertia", C.c_double * 9)]
 
 
 class Stats(C.Structure):
@@ -110,6 +116,12 @@ PROTOTYPES = {
     "mppi_target_rotation": (None, [_F, _F]),
     "mppi_savgol_coefficients": (C.c_int32, [C.c_int32, C.c_int32, _F]),
     "mppi_host_fk": (_ST, [C.POINTER(Joint), C.c_int32, _D, _D, C.c_int32, _F]),
+    "mppi_dyn_create": (_ST, [C.POINTER(Link), C.c_int32, C.c_double, C.POINTER(_P)]),
+    "mppi_dyn_destroy": (None, [_P]),
+    "mppi_dyn_dims": (None, [_P, _I32, _I32, _I32]),
+    "mppi_dyn_rnea": (_ST, [_P, _D, _D, _D, _D]),
+    "mppi_dyn_terms": (_ST, [_P, _D, _D, _D, _D]),
+    "mppi_computed_torque": (_ST, [_P, _D, _D, _D, C.c_double, C.c_double, C.c_int32, _D]),
     "mppi_philox_normals": (_ST, [C.c_uint64, C.c_uint32, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_int32, _F, _U32]),
 }

@@ -534,6 +534,8 @@ mppi_status validate(const mppi_config& c) {
 extern "C" {
 
 int32_t mppi_abi_version(void) { return MPPI_ABI_VERSION; }
+// error reporting for the host dynamics TU (mppi_dynamics.cpp); not in the public header
+mppi_status mppi_fail_dyn(mppi_status st, const char* msg) { return fail(st, "%s", msg); }
 const char* mppi_last_error(void) { return g_err.c_str(); }
 
 void mppi_struct_sizes(int32_t* c, int32_t* j, int32_t* s) {
