@@ -18,7 +18,12 @@ using namespace mppi;
 //   FINAL: w_eps = N/eta, SavGol (symmetric pad), u += w_eps, outputs written
 //          straight into mapped pinned host memory (no D2H copy).
 // =============================================================================
-constexpr int kFinThreads = 512;
+// Block size NT (template): the smallest of 128 / 256 / 512 threads whose one chunk of
+// loads covers every record (rows per chunk = NT * kNPT / CW), else 512.  Measured on
+// MI355X (profiles/r01/finalize_threads_s3.txt): arm C3 (256 records) 5.91 -> 5.26 us at
+// 256 threads, the V=8 fleet (128 records per vehicle) 10.58 -> 5.46 us at 128, whole-body
+// K=8192 (512 records) best at 512.
+constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 waves)
 constexpr int kMaxRec = 4096;
 
 // DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
@@ -77,14 +82,14 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 // finishes alone: w_eps, SavGol by lane shuffles (WIN taps, template), u_prev,
 // outputs.
 // The leading scalar arguments are preloaded into SGPRs (build.py).
-template <int CW, int WIN>
-__global__ void __launch_bounds__(kFinThreads) k_finalize(const float* __restrict__ hdr_base,
+template <int CW, int WIN, int NT>
+__global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_base,
                                                           const float* __restrict__ dat_base,
                                                           float* __restrict__ u_prev, const uint32_t nrec_H,
                                                           const uint32_t geo, const int32_t hdr_rs,
                                                           const int32_t d_rs, const int32_t d_as,
                                                           const FinParams pk) {
-    constexpr int NWV = kFinThreads / 64;
+    constexpr int NWV = NT / 64;
     constexpr int ROWS = 64 / CW;          // rows per wave
     constexpr int TR = NWV * ROWS;         // rows per block
     constexpr int kNPT = 16;
@@ -290,11 +295,21 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
         return -1;
     const uint32_t nh = (uint32_t)p->nrec | ((uint32_t)p->H << 16);
     const uint32_t geo = (uint32_t)p->tsz | ((uint32_t)p->half << 8) | ((uint32_t)p->ts << 16) | ((uint32_t)p->A << 24);
-    const dim3 grid(p->A * p->ts, p->V), block(kFinThreads);
+    const int cw = (W <= 16) ? 16 : (W <= 32) ? 32 : 64;
+    int nt = 512;
+    for (int c : {128, 256})
+        if (c * 16 / cw >= p->nrec) { nt = c; break; }
+    const dim3 grid(p->A * p->ts, p->V), block(nt);
     hipStream_t s = (hipStream_t)stream;
-#define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
-    hipLaunchKernelGGL((k_finalize<CWV, WINV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo,    \
+#define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
+    hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo, \
                        (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, *p)
+#define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
+    do {                                                                                                  \
+        if (nt == 128) MPPI_FIN_GO(CWV, WINV, 128);                                                       \
+        else if (nt == 256) MPPI_FIN_GO(CWV, WINV, 256);                                                  \
+        else MPPI_FIN_GO(CWV, WINV, 512);                                                                 \
+    } while (0)
 #define MPPI_FIN_WIN(CWV)                                                                                 \
     do {                                                                                                  \
         if (p->window == 9) MPPI_FIN_LAUNCH(CWV, 9);                                                      \
@@ -306,6 +321,7 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     else MPPI_FIN_WIN(64);
 #undef MPPI_FIN_WIN
 #undef MPPI_FIN_LAUNCH
+#undef MPPI_FIN_GO
     return (int)hipGetLastError();
 }
 
