@@ -298,7 +298,8 @@ def main():
                         "timing": tim["method"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "bytes_per_launch": r["bytes"]},
+                         "kernel": "k_rollout_quad" if r["cfg"].model == 3 else "k_rollout",
+                         "bytes_per_launch": r["bytes"]},
             "cpu_baseline": cpu,
             "secondary": secondary or None,
         }

@@ -12,6 +12,6 @@ timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_$tag.json 2> gpurun_ou
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$tag.json
 if [ $rc -ne 0 ]; then tail -20 gpurun_out/bench_$tag.err; exit $rc; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$tag -o run -- \
-    python3 bench.py --steps 300 --no-cpu-baseline --secondary "" "$@" > gpurun_out/prof_$tag.json 2> gpurun_out/prof_$tag.err
+    python3 bench.py --no-cpu-baseline --secondary "" --latency-steps 0 "$@" > gpurun_out/prof_$tag.json 2> gpurun_out/prof_$tag.err
 rc=$?; echo "prof rc=$rc"; cat gpurun_out/prof_$tag/run_kernel_stats.csv
 exit $rc

@@ -45,7 +45,7 @@ def main():
             allw = json.load(open(out))
         except (OSError, ValueError):
             allw = {}
-        roll = rec.get("k_rollout", {})
+        roll = next((rec[k] for k in sorted(rec) if k.startswith("k_rollout")), {})
         allw[workload] = {"hbm_bytes_per_launch": roll.get("hbm_bytes_per_launch"), "kernels": rec,
                           "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes, avg per dispatch"}
         json.dump(allw, open(out, "w"), indent=1)
