@@ -190,13 +190,15 @@ __device__ __forceinline__ void kin_joint(Mat34& T, const float* O, QT q) {
     }
     float s, c;
     sincos_joint(q, s, c);
-    const float omc = 1.0f - c, r22 = c + omc;   // Rodrigues about z (transformation_matrix.py:68-93)
+    // Rodrigues about z (transformation_matrix.py:68-93).  Its R22 = fl(c + fl(1 - c)) is
+    // 1 or 1 - 2^-24 (a rounding tie of 1 - c for some c < -1/2); the fast path takes 1,
+    // as it takes the origins' pi/2 rotations exactly (<= 6e-8 relative).
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float a0 = r.m[4 * i], a1 = r.m[4 * i + 1];
         T.m[4 * i] = a0 * c + a1 * s;
         T.m[4 * i + 1] = a1 * c - a0 * s;
-        T.m[4 * i + 2] = r.m[4 * i + 2] * r22;
+        T.m[4 * i + 2] = r.m[4 * i + 2];   // R22 = fl(c + fl(1 - c)) taken as 1
         T.m[4 * i + 3] = r.m[4 * i + 3];
     }
 }
@@ -285,20 +287,19 @@ __device__ __forceinline__ float seg_scan_f32(float x) {
 }
 
 
-// Trajectory stores (every wave store instruction writes 256 contiguous bytes).
-// MPPI_TRAJ_STORE selects the cache policy (experiment knob):
-// 0 plain, 1 nontemporal, 2 write-through (sc1).
-#ifndef MPPI_TRAJ_STORE
-#define MPPI_TRAJ_STORE 0
+// Trajectory stores (every wave store instruction writes 256 contiguous bytes).  The
+// planes of one vehicle are one buffer resource (C*K*H*4 < 4 GiB, checked at create):
+// the lane's byte offset sits in one VGPR and the plane offset in an SGPR, so a store
+// costs no 64-bit address arithmetic (a v_lshl_add_u64 per store with flat addresses).
+// MPPI_TRAJ_AUX is the store's cache-policy field (experiment knob, 0 = plain).
+#ifndef MPPI_TRAJ_AUX
+#define MPPI_TRAJ_AUX 0
 #endif
-__device__ __forceinline__ void traj_store(float* dst, float x) {
-#if MPPI_TRAJ_STORE == 1
-    __builtin_nontemporal_store(x, dst);
-#elif MPPI_TRAJ_STORE == 2
-    __hip_atomic_store(dst, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *dst = x;
-#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t traj_rsrc(float* planes_v, uint32_t plane_b, int C) {
+    return __builtin_amdgcn_make_buffer_rsrc(planes_v, 0, (int)(plane_b * (uint32_t)C), 0x00020000);
+}
+__device__ __forceinline__ void traj_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, float x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)voff, (int)soff, MPPI_TRAJ_AUX);
 }
 
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
@@ -440,6 +441,11 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
     const int H = H_arg, K = pk.K;
     STAMP(1);
 
+    // trajectory planes of vehicle v (from kernel arguments and blockIdx only, so the
+    // descriptor stays in SGPRs)
+    const uint32_t plane_b = (uint32_t)K * (uint32_t)H * 4u;
+    const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * K * H, plane_b, pk.C);
+
     float acc[NCH][NA];
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -453,8 +459,6 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
     auto group = [&](const int it) {
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
-        const int plane_i = K * H;
-        float* traj_base = pk.traj;
         const int g = blockIdx.x + it * p.nb;
         const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
@@ -600,15 +604,14 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
             const bool val = kval && t < H;
             const bool term = (t == H - 1);
             float x;
-            const size_t plane = (size_t)plane_i;
-            float* tdst = traj_base + ((size_t)v * p.C * K + k) * H + t;
+            const uint32_t toff = ((uint32_t)k * (uint32_t)H + (uint32_t)t) * 4u;   // byte offset in a plane
             if (MODEL == MPPI_MODEL_DRONE) {
                 const float dx = posf[c][0] - vc.tpos[0], dy = posf[c][1] - vc.tpos[1],
                             dz = posf[c][2] - vc.tpos[2];
                 x = dx * dx + dy * dy + dz * dz;
                 if (p.store_traj && val) {
-                    traj_store(tdst, posf[c][0]); traj_store(tdst + plane, posf[c][1]);
-                    traj_store(tdst + 2 * plane, posf[c][2]);
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
                 }
             } else {
                 // joint angle j in the state dtype (fp64 state -> fp64 sin/cos reduction)
@@ -674,9 +677,9 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 x = pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
                 if (p.store_traj && val) {
 #pragma unroll
-                    for (int a = 0; a < NA; ++a) traj_store(tdst + a * plane, posf[c][a]);
+                    for (int a = 0; a < NA; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) traj_store(tdst + (NA + i) * plane, T.m[i]);
+                    for (int i = 0; i < 12; ++i) traj_store(trs, toff, (uint32_t)(NA + i) * plane_b, T.m[i]);
                 }
             }
             xs[c] = val ? x : 0.0f;
@@ -817,9 +820,15 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
         }
         *reinterpret_cast<float4*>(p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4) = make_float4(rho_b, eta, eta2, nanf);
     }
-    // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t]
+    // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t].
+    // (a, t) of element i without an integer division (~25 VALU): a = trunc((i + 1/2) / H)
+    // in fp32 is exact, the quotient's error (< 1e-5 for i < A*H <= 2560) being far below
+    // the 1/(2H) margin; 32-bit record indices (V*A*nb*H < 2^31, checked at create).
+    const float rH = 1.0f / (float)H;
+    const uint32_t rbase = ((uint32_t)v * NA * (uint32_t)p.nb + blockIdx.x) * (uint32_t)H;
+    const uint32_t rstride = (uint32_t)p.nb * (uint32_t)H;
     for (int i = tid; i < HA; i += nthr) {
-        const int a = i / H, t = i - a * H;
+        const int a = (int)(((float)i + 0.5f) * rH), t = i - a * H;
         const int c = t >> 6, tl = t & 63;
         float s = 0.0f;
 #pragma unroll
@@ -829,7 +838,7 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
             for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
             s += fw[w] * sw;
         }
-        p.rdata[(((size_t)v * NA + a) * p.nb + blockIdx.x) * H + t] = s;
+        p.rdata[rbase + (uint32_t)a * rstride + (uint32_t)t] = s;
     }
     STAMP(7);
 }

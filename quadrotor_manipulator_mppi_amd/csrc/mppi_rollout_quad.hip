@@ -128,8 +128,9 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
         // trajectory planes t-major, (V, C, H, K): lane = rollout, so each store instruction
         // of a step writes 64 consecutive floats (the (V,C,K,H) planes of k_rollout would
         // scatter them H floats apart)
-        const size_t plane = (size_t)K * H;
-        float* tdst = p.traj + (size_t)v * p.C * plane + k;
+        const uint32_t plane_b = (uint32_t)K * (uint32_t)H * 4u;
+        const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * K * H, plane_b, pk.C);
+        const uint32_t koff = (uint32_t)k * 4u, tstep_b = (uint32_t)K * 4u;
         float stage = 0.0f, term = 0.0f;
         // one step; the first (FIRST) is peeled: it integrates the measured velocity and
         // rates (drone_mppi.py:65-70) and skips the angle wrap
@@ -177,9 +178,10 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
             vx = nvx; vy = nvy; vz = nvz;
             er = nr; ep = np_; ey = ny;
             if (p.store_traj && kval) {
-                float* d = tdst + (size_t)t * K;
-                traj_store(d, px); traj_store(d + plane, py); traj_store(d + 2 * plane, pz);
-                traj_store(d + 3 * plane, er); traj_store(d + 4 * plane, ep); traj_store(d + 5 * plane, ey);
+                const uint32_t o = koff + (uint32_t)t * tstep_b;
+                traj_store(trs, o, 0u, px); traj_store(trs, o, plane_b, py); traj_store(trs, o, 2u * plane_b, pz);
+                traj_store(trs, o, 3u * plane_b, er); traj_store(trs, o, 4u * plane_b, ep);
+                traj_store(trs, o, 5u * plane_b, ey);
             }
             // squared position error (drone_mppi.py:87-107)
             const float dx = px - tx, dy = py - ty, dz = pz - tz;
