@@ -1403,7 +1403,7 @@ mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, i
         return fail(MPPI_ERR_INVALID_ARG, "mppi_philox_normals: bad arguments");
     HIP_TRY(hipSetDevice(device));
     const size_t n = (size_t)K * H;
-    const int nj = (A + 3) / 4;
+    const int nj = (A + 7) / 8;   // Philox calls per (k, t): 8 normals each
     float* dz = nullptr;
     uint32_t* dr = nullptr;
     HIP_TRY(hipMalloc(&dz, n * A * sizeof(float)));

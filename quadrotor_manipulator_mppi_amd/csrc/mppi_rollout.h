@@ -19,6 +19,12 @@
 #pragma once
 #include "mppi_device.h"
 
+// Timing knockouts for tools/ experiments only (MPPI_HIPCC_EXTRA=-DMPPI_KO=n; results are
+// wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain.
+#ifndef MPPI_KO
+#define MPPI_KO 0
+#endif
+
 namespace {
 
 // ------------------------------------------------------------------- Philox
@@ -52,33 +58,38 @@ __device__ __forceinline__ float uniform_f32(float x) {   // wave-uniform value 
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
 
-__device__ __forceinline__ float u01(uint32_t x) {   // (0,1), exact in fp32
-    return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f;
-}
-
-// Box-Muller on the hardware transcendental units: v_log_f32 (log2),
-// v_sqrt_f32, v_sin_f32 / v_cos_f32 (argument in revolutions).
-__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-    const float u1 = u01(a), u2 = u01(b);
+// One standard-normal pair per 32-bit Philox word (Box-Muller on the hardware
+// transcendental units: v_log_f32 (log2), v_sqrt_f32, v_sin_f32 / v_cos_f32 with the
+// argument in revolutions).  The radius takes the top 18 bits, u1 = (w>>14 + 1/2) 2^-18,
+// the angle the low 14, u2 = ((w & 0x3fff) + 1/2) 2^-14 (midpoint grids: the radial CDF
+// is off by <= 2^-19, the angle's midpoint rule by O(2^-28); the tail is cut at 5.1
+// sigma, mass 3e-7).  One Philox4x32-10 call thus yields 8 normals: the 7 arm dims take
+// one call and the 10 whole-body dims two (two words per pair took 2 and 3).
+__device__ __forceinline__ void box_muller32(uint32_t w, float& z0, float& z1) {
+    const float u1 = ((float)(w >> 14) + 0.5f) * 3.814697265625e-6f;      // 2^-18
+    const float u2 = ((float)(w & 0x3FFFu) + 0.5f) * 6.103515625e-5f;     // 2^-14
     const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
     z0 = r * __builtin_amdgcn_cosf(u2);
     z1 = r * __builtin_amdgcn_sinf(u2);
 }
 
+// z[a] for a < NA: Philox call j (counter (kg, t, veh<<8 | j, step)) gives normals
+// 8j .. 8j+7, word i of it the pair (8j+2i, 8j+2i+1).
 template <int NA>
 __device__ __forceinline__ void draw_normals(float (&z)[NA], uint32_t kg, uint32_t t, uint32_t veh,
                                              uint32_t step, uint32_t s0, uint32_t s1) {
 #pragma unroll
-    for (int j = 0; j < (NA + 3) / 4; ++j) {
-        uint32_t c0 = kg, c1 = t, c2 = (veh << 8) | (uint32_t)j, c3 = step;
-        philox10(c0, c1, c2, c3, s0, s1);
-        float a, b, c, d;
-        box_muller(c0, c1, a, b);
-        box_muller(c2, c3, c, d);
-        if (4 * j + 0 < NA) z[4 * j + 0] = a;
-        if (4 * j + 1 < NA) z[4 * j + 1] = b;
-        if (4 * j + 2 < NA) z[4 * j + 2] = c;
-        if (4 * j + 3 < NA) z[4 * j + 3] = d;
+    for (int j = 0; j < (NA + 7) / 8; ++j) {
+        uint32_t w[4] = {kg, t, (veh << 8) | (uint32_t)j, step};
+        if (!(MPPI_KO & 2)) philox10(w[0], w[1], w[2], w[3], s0, s1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (8 * j + 2 * i >= NA) break;
+            float a, b;
+            box_muller32(w[i], a, b);
+            z[8 * j + 2 * i] = a;
+            if (8 * j + 2 * i + 1 < NA) z[8 * j + 2 * i + 1] = b;
+        }
     }
 }
 
@@ -308,6 +319,7 @@ __device__ __forceinline__ void traj_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
 // bound_ctrl) or rows outside row_mask add 0 (row_bcast), so no zeroing moves.
 template <int L, int NA>
 __device__ __forceinline__ void seg_scan_f32_multi(float (&x)[NA]) {
+    if (MPPI_KO & 1) return;
 #define MPPI_SCAN_STEP(CTRL, RM, BC)                                                    \
     _Pragma("unroll") for (int a = 0; a < NA; ++a) x[a] += __int_as_float(             \
         __builtin_amdgcn_update_dpp(0, __float_as_int(x[a]), CTRL, RM, 0xF, BC));
@@ -624,7 +636,9 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 if (MODEL == MPPI_MODEL_WHOLEBODY) {   // [R(rpy) | p_drone(k,t)] * M_fixed
                     T.m[3] += posf[c][0]; T.m[7] += posf[c][1]; T.m[11] += posf[c][2];
                 }
-                if (NQ == 7 && p.chain_fast == 2) {   // Kinova: origin rotations are signed permutations
+                if (MPPI_KO & 4) {
+                    T.m[3] += posf[c][QOFF]; T.m[7] += posf[c][QOFF + 1];
+                } else if (NQ == 7 && p.chain_fast == 2) {   // Kinova: origin rotations are signed permutations
                     kin_joint<0>(T, jnt[p.j0 + 0].O, qang(c, 0));
                     kin_joint<1>(T, jnt[p.j0 + 1].O, qang(c, 1));
                     kin_joint<2>(T, jnt[p.j0 + 2].O, qang(c, 2));

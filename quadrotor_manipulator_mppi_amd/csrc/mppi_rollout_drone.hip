@@ -6,18 +6,20 @@ __global__ void k_philox(uint64_t seed, uint32_t step, int veh, int64_t k0, int 
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= K * H) return;
     const int k = i / H, t = i - k * H;
-    const int nj = (A + 3) / 4;
+    const int nj = (A + 7) / 8;   // one Philox call per 8 normals (box_muller32: one pair per word)
     for (int j = 0; j < nj; ++j) {
         uint32_t c0 = (uint32_t)(k0 + k), c1 = (uint32_t)t, c2 = ((uint32_t)veh << 8) | (uint32_t)j, c3 = step;
         philox10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
         uint32_t* rw = raw + ((size_t)i * nj + j) * 4;
         rw[0] = c0; rw[1] = c1; rw[2] = c2; rw[3] = c3;
-        float n0, n1, n2, n3;
-        box_muller(c0, c1, n0, n1);
-        box_muller(c2, c3, n2, n3);
-        const float nn[4] = {n0, n1, n2, n3};
-        for (int q = 0; q < 4; ++q)
-            if (4 * j + q < A) z[(size_t)i * A + 4 * j + q] = nn[q];
+        const uint32_t wv[4] = {c0, c1, c2, c3};
+        for (int q = 0; q < 4; ++q) {
+            float n0, n1;
+            box_muller32(wv[q], n0, n1);
+            const int a = 8 * j + 2 * q;
+            if (a < A) z[(size_t)i * A + a] = n0;
+            if (a + 1 < A) z[(size_t)i * A + a + 1] = n1;
+        }
     }
 }
 

@@ -168,8 +168,17 @@ def test_philox_known_answer():
 
 
 def test_philox_normals_moments():
-    raw, z = O.philox_normals(1234, 0, 0, np.arange(4096), 32, 4)
-    z = z.astype(np.float64).ravel()
-    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    """The device mapping (one Box-Muller pair per Philox word, 18-bit radius, 14-bit
+    angle): per-dim moments, a KS test on 2e5 draws, no cross-dim correlation."""
     from scipy import stats
-    assert stats.kstest(z[:20000], "norm").pvalue > 1e-3
+    for A in (4, 7, 10):
+        raw, z = O.philox_normals(1234, 0, 0, np.arange(2048), 32, A)
+        assert raw.shape == (2048, 32, 4 * ((A + 7) // 8))
+        z = z.astype(np.float64).reshape(-1, A)
+        assert np.all(np.abs(z.mean(0)) < 0.01) and np.all(np.abs(z.std(0) - 1.0) < 0.01)
+        c = np.corrcoef(z.T) - np.eye(A)
+        assert np.abs(c).max() < 5.0 / np.sqrt(len(z))   # 5 sigma of a null correlation estimate
+        assert stats.kstest(z[:20000].ravel(), "norm").pvalue > 1e-3
+        assert np.abs(z).max() < 5.2            # the 18-bit radius cuts the tail at 5.13 sigma
+    raw, z = O.philox_normals(99, 3, 1, np.arange(20000), 10, 2)
+    assert stats.kstest(z.ravel().astype(np.float64), "norm").pvalue > 1e-3
