@@ -20,9 +20,14 @@
 #include "mppi_device.h"
 
 // Timing knockouts for tools/ experiments only (MPPI_HIPCC_EXTRA=-DMPPI_KO=n; results are
-// wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain.
+// wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain,
+// 8 the pose cost, 16 the trajectory stores, 32 Box-Muller, 64 the block record body.
 #ifndef MPPI_KO
 #define MPPI_KO 0
+#endif
+// waves per SIMD the rollout kernel is register-budgeted for (4: <= 128 VGPRs)
+#ifndef MPPI_ROLL_OCC
+#define MPPI_ROLL_OCC 4
 #endif
 
 namespace {
@@ -66,6 +71,7 @@ __device__ __forceinline__ float uniform_f32(float x) {   // wave-uniform value 
 // sigma, mass 3e-7).  One Philox4x32-10 call thus yields 8 normals: the 7 arm dims take
 // one call and the 10 whole-body dims two (two words per pair took 2 and 3).
 __device__ __forceinline__ void box_muller32(uint32_t w, float& z0, float& z1) {
+    if (MPPI_KO & 32) { z0 = __uint_as_float((w & 0x3FFFFFu) | 0x3F800000u); z1 = z0 - 1.5f; return; }
     const float u1 = ((float)(w >> 14) + 0.5f) * 3.814697265625e-6f;      // 2^-18
     const float u2 = ((float)(w & 0x3FFFu) + 0.5f) * 6.103515625e-5f;     // 2^-14
     const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
@@ -165,21 +171,45 @@ __device__ __forceinline__ void sincos_poly(float x, int qd, float& s, float& c)
     if ((qd + 1) & 2) c = -c;
 }
 
+// Default: reduce the angle to f in [-1/2, 1/2] revolutions in the angle's own precision,
+// then the hardware v_sin_f32 / v_cos_f32 of 2 pi f (2 transcendentals + 4 ops instead of
+// ~20).  Measured on MI355X over random angles in [-3 pi, 3 pi]
+// (tools/microbench7.hip, profiles/r01/sincos_accuracy.txt): max error 1.8e-7 (fp64
+// angle) and 2.6e-7 (fp32 angle) absolute, vs 9e-8 for the polynomials -- 1e2 below the
+// trajectory tolerances.  MPPI_SINCOS_POLY=1 selects the polynomials.
+#ifndef MPPI_SINCOS_POLY
+#define MPPI_SINCOS_POLY 0
+#endif
 __device__ __forceinline__ void sincos_joint(double q, float& s, float& c) {
-    const double n = rint(q * 0.63661977236758134308);
-    double r = fma(-n, 1.5707963267948966192, q);
-    r = fma(-n, 6.123233995736766036e-17, r);
-    sincos_poly((float)r, (int)n, s, c);
+    if (MPPI_SINCOS_POLY) {
+        const double n = rint(q * 0.63661977236758134308);
+        double r = fma(-n, 1.5707963267948966192, q);
+        r = fma(-n, 6.123233995736766036e-17, r);
+        sincos_poly((float)r, (int)n, s, c);
+        return;
+    }
+    const double r = q * 0.15915494309189533577;
+    const float f = (float)(r - rint(r));
+    s = __builtin_amdgcn_sinf(f);
+    c = __builtin_amdgcn_cosf(f);
 }
 
-// fp32 state (torch.sin of a float32 tensor): the same polynomials after a
-// two-constant fp32 Cody-Waite reduction (pi/2 = PIO2_HI + PIO2_MID; the
-// dropped tail is 1.8e-15 * n), no fp64 work.
+// fp32 state (torch.sin of a float32 tensor): 1/2pi = C_HI + C_LO, the fractional
+// revolution by two FMAs (the polynomial path: a two-constant Cody-Waite reduction by
+// pi/2, the dropped tail 1.8e-15 * n).
 __device__ __forceinline__ void sincos_joint(float q, float& s, float& c) {
-    const float n = __builtin_rintf(q * 0.636619772367581343f);
-    float r = fmaf(-n, 1.5707963705062866f, q);
-    r = fmaf(-n, -4.371138828673793e-08f, r);
-    sincos_poly(r, (int)n, s, c);
+    if (MPPI_SINCOS_POLY) {
+        const float n = __builtin_rintf(q * 0.636619772367581343f);
+        float r = fmaf(-n, 1.5707963705062866f, q);
+        r = fmaf(-n, -4.371138828673793e-08f, r);
+        sincos_poly(r, (int)n, s, c);
+        return;
+    }
+    const float n = __builtin_rintf(q * 0.15915494309189535f);
+    float f = fmaf(q, 0.15915494309189535f, -n);
+    f = fmaf(q, 6.4206382e-09f, f);
+    s = __builtin_amdgcn_sinf(f);
+    c = __builtin_amdgcn_cosf(f);
 }
 
 // One Kinova joint: T <- T * [P | o] * Rz(q), P a signed permutation fixed at
@@ -310,6 +340,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t traj_rsrc(float* planes_v, uin
     return __builtin_amdgcn_make_buffer_rsrc(planes_v, 0, (int)(plane_b * (uint32_t)C), 0x00020000);
 }
 __device__ __forceinline__ void traj_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, float x) {
+    if (MPPI_KO & 16) return;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)voff, (int)soff, MPPI_TRAJ_AUX);
 }
 
@@ -357,7 +388,7 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
 // draw and the u_prev / joint-table loads start without waiting for the
 // kernel-argument segment (its first s_load costs ~1.5k cycles).
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC>
-__global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+__global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
                                                  const int32_t nthr,
@@ -688,7 +719,7 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
                 // addresses per lane would otherwise become two vector loads in the FK
                 const float wsp = uniform_f32(p.w_sp), wso = uniform_f32(p.w_so), wtp = uniform_f32(p.w_tp),
                             wto = uniform_f32(p.w_to);
-                x = pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
+                x = (MPPI_KO & 8) ? T.m[3] + T.m[7] + T.m[11] + T.m[0] : pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
                 if (p.store_traj && val) {
 #pragma unroll
                     for (int a = 0; a < NA; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
@@ -841,7 +872,7 @@ __global__ void __launch_bounds__(512, 4) k_rollout(const uint32_t seed_lo, cons
     const float rH = 1.0f / (float)H;
     const uint32_t rbase = ((uint32_t)v * NA * (uint32_t)p.nb + blockIdx.x) * (uint32_t)H;
     const uint32_t rstride = (uint32_t)p.nb * (uint32_t)H;
-    for (int i = tid; i < HA; i += nthr) {
+    for (int i = tid; i < ((MPPI_KO & 64) ? 0 : HA); i += nthr) {
         const int a = (int)(((float)i + 0.5f) * rH), t = i - a * H;
         const int c = t >> 6, tl = t & 63;
         float s = 0.0f;
