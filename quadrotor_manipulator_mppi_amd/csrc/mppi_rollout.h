@@ -613,7 +613,9 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                         c1[a] += carry1[a];
                         carry1[a] = read_lane_f32(c1[a], 63);
                     }
-                    const float h2 = (0.5f * act[c][a]) * p.dt2;
+                    // (0.5 a) dt^2 == a (0.5 dt^2) bit for bit: both are one rounding of the
+                    // same product, the halvings being exact
+                    const float h2 = act[c][a] * (0.5f * p.dt2);
                     const float velf = c1[a] + vc.vel0f[a];
                     float prev = dpp_f32<0x138, 0xF>(velf);     // wave_shr:1
                     if (t0 == 0) prev = (c == 0) ? vc.vel0f[a] : lastv[a];
