@@ -383,6 +383,89 @@ __device__ __forceinline__ float seg_pick(float x, int sub, int l_in_seg, int L)
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// Integrator in the transposed domain (NCH == 1).  The two cumsums of
+// standard_normal_noise.py:41-48 as DPP scans cost 13 DPP ops per dim and lane
+// (row_shr 1/2/4/8, row_bcast 15/31, wave_shr 1).  Instead the wave writes its
+// controls to its LDS slot (row = lane = (segment, t), pitch P = NA rounded up to odd,
+// so the transposed reads are bank-conflict free) and re-reads them with lane =
+// (series = (segment, dim), chunk of CL consecutive t).  Each lane integrates its chunk
+// sequentially (4 full-rate ops per element), the chunks of a series combine by an
+// affine exclusive scan over CPS consecutive lanes (2 log2 CPS + 2 DPP moves), and the
+// position increments go back through LDS to lane = t.  For a chunk starting at
+// velocity V and position P (relative to q0, q0dot), element i:
+//   dq(i) = P + lp(i) + (i + 1) dt V,   lp(i) = sum_{j <= i} (lv(j) dt + a_j dt^2 / 2),
+//   lv(j) = sum_{m < j} a_m dt;   combine(L then R) : V = V_L + V_R,
+//   P = P_L + P_R + n_R dt V_L  (n_R elements in R).
+// q0dot enters as (t + 1) dt q0dot.  fp32 throughout (the old scans were fp32 too); the
+// increments stay ~1e-10 from the reference's double-accumulated cumsums.
+template <int L, int NA>
+struct IntegGeom {
+    static constexpr int R = 64 / L;
+    static constexpr int S = R * NA;   // series per wave
+    static constexpr int CPS = (S <= 4) ? 16 : (S <= 8) ? 8 : (S <= 16) ? 4 : (S <= 32) ? 2 : 1;
+    static constexpr int CL = L / CPS;   // elements per chunk
+    static constexpr int P = NA | 1;     // LDS row pitch (odd)
+    static_assert(S * CPS <= 64 && CPS <= L, "integrator lane map");
+};
+
+// floats per wave slot in LDS: the block-combine deposit (4 + NCH*64*NA) and, for
+// NCH == 1, the integrator's 64 x P transposition buffer
+template <int NA, int NCH, int L>
+constexpr int wave_slot_floats() {
+    return (NCH == 1 && 64 * IntegGeom<L, NA>::P > 4 + NCH * 64 * NA) ? 64 * IntegGeom<L, NA>::P
+                                                                     : 4 + NCH * 64 * NA;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float row_shr_f32(float x) {   // out-of-row sources read 0
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+
+// inc[a] (lane = segment*L + t) = q(t) - q0 for the controls act[a] of this lane
+template <int L, int NA>
+__device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw, const int lane, const float dt,
+                                              const float dt2h, const float* vel0f, float (&inc)[NA]) {
+    using G = IntegGeom<L, NA>;
+    constexpr int P = G::P, CPS = G::CPS, CL = G::CL, S = G::S;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) xw[lane * P + a] = act[a];
+    asm volatile("" ::: "memory");   // a wave's LDS ops execute in order: no wait needed
+    const int sr = lane / CPS, ch = lane & (CPS - 1);
+    const bool on = sr < S;
+    const int seg = sr / NA, a = sr - seg * NA;
+    const int rb = on ? (seg * L + ch * CL) * P + a : 0;
+    float lv = 0.0f, lp = 0.0f, loc[CL];
+#pragma unroll
+    for (int i = 0; i < CL; ++i) {
+        const float x = xw[rb + i * P];
+        lp += fmaf(lv, dt, x * dt2h);
+        lv = fmaf(x, dt, lv);
+        loc[i] = lp;
+    }
+    // inclusive affine scan over the series' chunks (consecutive lanes of one DPP row)
+    float V = lv, Q = lp;
+#define MPPI_ISCAN(D, CTRL)                                                                if (CPS > D) {                                                                             const float vs = row_shr_f32<CTRL>(V), qs = row_shr_f32<CTRL>(Q);                       if (ch >= D) { Q = Q + fmaf((float)(D * CL) * dt, vs, qs); V = V + vs; }            }
+    MPPI_ISCAN(1, 0x111)
+    MPPI_ISCAN(2, 0x112)
+    MPPI_ISCAN(4, 0x114)
+    MPPI_ISCAN(8, 0x118)
+#undef MPPI_ISCAN
+    float Vx = row_shr_f32<0x111>(V), Qx = row_shr_f32<0x111>(Q);   // exclusive: previous chunk's
+    if (ch == 0) { Vx = 0.0f; Qx = 0.0f; }
+    const float v0 = on ? vel0f[a] : 0.0f;
+    const float q0 = fmaf((float)(ch * CL) * dt, v0, Qx);   // chunk start incl. the q0dot drift
+    const float vb = dt * (Vx + v0);
+    asm volatile("" ::: "memory");
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < CL; ++i) xw[rb + i * P] = fmaf((float)(i + 1), vb, q0 + loc[i]);
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int a2 = 0; a2 < NA; ++a2) inc[a2] = xw[lane * P + a2];
+}
+
 // The leading scalar arguments are preloaded into SGPRs at wave launch on gfx950
 // (-mllvm -amdgpu-kernarg-preload-count, build.py): the first group's Philox
 // draw and the u_prev / joint-table loads start without waiting for the
@@ -482,6 +565,8 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
     const VehicleConst& vc = vcv;
     const float* sdiag = pk.sdiag;
     const int H = H_arg, K = pk.K;
+    constexpr int kWs = wave_slot_floats<NA, NCH, LSEG>();
+    float* const xw = smem + ((HA + 3) & ~3) + wid * kWs;   // this wave's LDS slot
     STAMP(1);
 
     // trajectory planes of vehicle v (from kernel arguments and blockIdx only, so the
@@ -596,7 +681,19 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
         //      dtype (fp64 state -> fp64 positions, as update_joint's float64 arrays).
         float posf[NCH][NA];
         double posd[NCH][F64 ? NA : 1];
-        {
+        if constexpr (NCH == 1 && !(MPPI_KO & 1)) {
+            float inc[NA];
+            integrate_lds<LSEG, NA>(act[0], xw, lane, p.dt, 0.5f * p.dt2, vc.vel0f, inc);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                if (!F64) {
+                    posf[0][a] = inc[a] + vc.pos0f[a];
+                } else {
+                    posd[0][a] = (double)inc[a] + vc.pos0[a];
+                    posf[0][a] = (float)posd[0][a];
+                }
+            }
+        } else {
 #pragma clang fp contract(off)
             float carry1[NA], carry2[NA], lastv[NA];
 #pragma unroll
@@ -834,7 +931,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
     //      rescales the 8 wave slots itself (f_w = exp(-(rho_w - rho_b)/lambda)).
     //      LDS: [8][4 + NCH*64*NA]; every lane (all R segments) deposits acc
     float* wsh = smem + ((HA + 3) & ~3);           // always 8 wave slots (unrolled reads)
-    const int wstride = 4 + NCH * 64 * NA;
+    const int wstride = kWs;   // >= 4 + NCH*64*NA (the integrator's buffer may be larger)
     float* mine = wsh + wid * wstride;
     if (lane == 0) {
         mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f;
@@ -895,7 +992,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
 // =============================================================================
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
 inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
-    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * (4 + NCH * 64 * NA)) * sizeof(float);
+    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>()) * sizeof(float);
     if (p.V == 1)
         hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC>), dim3(p.nb, p.V), dim3(threads), lds, s,
                            p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
