@@ -27,7 +27,7 @@ LIB_STAMPS = os.path.join(LIB_DIR, "libmppi_hip_stamps.so")   # diagnostic phase
 # are preloaded into SGPRs at wave launch.
 _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
 SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
-           ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=11"]),
+           ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=13"]),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", [])]
 HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", os.path.join("..", "..", "include", "mppi_hip.h")]
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")

@@ -81,13 +81,15 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 // (xor shuffles, DPP), the 8 waves through LDS behind ONE barrier, and wave 0
 // finishes alone: w_eps, SavGol by lane shuffles (WIN taps, template), u_prev,
 // outputs.
-// The leading scalar arguments are preloaded into SGPRs (build.py).
+// The leading scalar arguments (through the vehicle-constant pointer) are preloaded into
+// SGPRs (build.py: 13 dwords).
 template <int CW, int WIN, int NT>
 __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_base,
                                                           const float* __restrict__ dat_base,
                                                           float* __restrict__ u_prev, const uint32_t nrec_H,
                                                           const uint32_t geo, const int32_t hdr_rs,
                                                           const int32_t d_rs, const int32_t d_as,
+                                                          const VehicleConst* __restrict__ vcs,
                                                           const FinParams pk) {
     constexpr int NWV = NT / 64;
     constexpr int ROWS = 64 / CW;          // rows per wave
@@ -117,8 +119,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     float x0f = 0.0f, v0f = 0.0f;
     double x0d = 0.0, v0d = 0.0;
     if (tid == 0 && sl == 0) {
-        const VehicleConst& vc = p.vc[v];
-        x0f = vc.pos0f[a]; v0f = vc.vel0f[a]; x0d = vc.pos0[a]; v0d = vc.vel0[a];
+        // vector loads (a VGPR offset the compiler cannot prove uniform): scalar loads of
+        // these fields were waited for on the spot, two dependent s_load round trips
+        // ahead of the record loads
+        int vz;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+        const VehicleConst* vcp = vcs + v + vz;   // vcs == p.vc, a preloaded argument
+        x0f = vcp->pos0f[a]; v0f = vcp->vel0f[a]; x0d = vcp->pos0[a]; v0d = vcp->vel0[a];
     }
 
     float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
@@ -126,15 +133,20 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     for (int base = 0; base < n; base += TR * kNPT) {
         float4 hd[kNPT];
         float xv[kNPT];
+        uint32_t okm = 0;   // rows past n load row 0 and are masked at use: a select on the
+                            // loaded value here made the compiler wait for each load in turn
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
             const int r = base + gr + i * TR;
             const bool ok = r < n;
-            const size_t rr = (size_t)(ok ? r : 0);
-            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (size_t)hdr_rs);
-            xv[i] = col[rr * (size_t)d_rs + (qv ? q : 0)];
-            if (!ok) hd[i] = make_float4(INFINITY, 0.f, 0.f, 0.f);
+            okm |= (uint32_t)ok << i;
+            const uint32_t rr = (uint32_t)(ok ? r : 0);   // 32-bit offsets (nrec <= 4096)
+            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
+            xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
         }
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i)
+            if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
         FSTAMP(7);
         float m = INFINITY;
 #pragma unroll
@@ -303,7 +315,7 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     hipStream_t s = (hipStream_t)stream;
 #define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
     hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo, \
-                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, *p)
+                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, p->vc, *p)
 #define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
     do {                                                                                                  \
         if (nt == 128) MPPI_FIN_GO(CWV, WINV, 128);                                                       \

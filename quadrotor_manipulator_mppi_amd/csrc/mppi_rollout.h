@@ -760,6 +760,10 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                 auto qang = [&](int cc_, int j) {
                     if constexpr (F64) return posd[cc_][QOFF + j]; else return posf[cc_][QOFF + j];
                 };
+                if (p.store_traj && val) {   // positions first: each dies after its joint's FK step
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
+                }
                 Mat34 T;   // base (times the folded leading fixed joints)
 #pragma unroll
                 for (int i = 0; i < 12; ++i) T.m[i] = vc.base[i];
@@ -820,8 +824,6 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                             wto = uniform_f32(p.w_to);
                 x = (MPPI_KO & 8) ? T.m[3] + T.m[7] + T.m[11] + T.m[0] : pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
                 if (p.store_traj && val) {
-#pragma unroll
-                    for (int a = 0; a < NA; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
 #pragma unroll
                     for (int i = 0; i < 12; ++i) traj_store(trs, toff, (uint32_t)(NA + i) * plane_b, T.m[i]);
                 }
