@@ -148,9 +148,10 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
             sincos_joint(er, sr, cr);
             sincos_joint(ep, sp, cp);
             sincos_joint(ey, sy, cy);
-            // one IEEE reciprocal for tan and the 1/cos terms of J; mul/add pairs contract
-            // into FMAs (the dynamics are one wave's issue-bound chain)
-            const float ic = 1.0f / cp;
+            // one hardware reciprocal (v_rcp_f32, <= 1 ulp) for tan and the 1/cos terms of J:
+            // the IEEE division was ~10 ops on the one wave's serial chain; mul/add pairs
+            // contract into FMAs (the dynamics are that chain's issue)
+            const float ic = __builtin_amdgcn_rcpf(cp);
             const float tp = sp * ic;
             const float r02 = cy * sp * cr + sy * sr;
             const float r12 = sy * sp * cr - cy * sr;
