@@ -447,3 +447,51 @@ def test_sharded_engine_two_ranks_gloo():
     # 20 more closed-loop steps: the two combine orders' fp32 rounding feeds back
     # through u_prev, so the bar is the drift of the loop, not one step's rounding
     _close(res[0][1][3], ref[3], rtol=5e-3, atol=1e-4, what="after 23 steps")
+
+
+# ------------------------------------------- integrator lane maps (LDS transposition)
+@pytest.mark.parametrize("H,f64", [(16, True), (32, False), (48, True), (64, False), (64, True)])
+def test_arm_horizons_match_oracle(H, f64):
+    """The transposed integrator's lane maps (L = 32: 2 rollouts x 7 dims x 4 chunks of 8;
+    L = 64: 7 dims x 8 chunks of 8) with nonzero joint rates, fp32 and fp64 state."""
+    from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain
+    chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
+    K = 512
+    torch.manual_seed(100 + H)
+    noise = O.draw_noise(K, H, torch.eye(7) * 0.1)
+    u_prev = torch.randn(H, 7) * 0.3
+    q_full = np.array([0.1, -0.2, 1.1, 0.0, 0.0, 0.2588190, 0.9659258] + [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0])
+    v_full = np.array([0.0] * 6 + [0.8, -0.5, 0.3, -1.2, 0.4, 0.9, -0.7])
+    r = O.arm_step(chain, q_full, v_full, u_prev, noise, [0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5],
+                   f64=f64)
+    e = _engine(model="arm", n_samples=K, n_horizon=H, noise="injected", state_f64=f64)
+    e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    e.set_u_prev(u_prev.numpy())
+    e.step(np.concatenate([q_full[:7], q_full[7:], v_full[6:]]), noise.numpy()[None])
+    tr = e.get_trajectory()[0]
+    _close(tr[..., :7], r["q_samples"].numpy(), atol=2e-6, what="q")
+    _close(tr[..., 7:], r["ee"].numpy().reshape(K, H, 16), atol=2e-5, what="EE")
+    _close(e.get_costs()[0], r["S"].numpy(), rtol=2e-5, what="S")
+
+
+@pytest.mark.parametrize("H", [16, 32, 64])
+def test_wholebody_integrator_lane_maps(H):
+    """Whole-body positions (drone xyz + 7 joints) against the oracle integrator, incl.
+    L = 32 with 2 rollouts x 10 dims x 2 chunks of 16 per wave."""
+    K = 256
+    torch.manual_seed(200 + H)
+    sigma = torch.diag(torch.tensor([30.0] * 3 + [0.1] * 7))
+    noise = O.draw_noise(K, H, sigma)
+    u_prev = torch.randn(H, 10) * 0.3
+    x, vx = [0.3, -0.1, 1.2], [0.5, -0.4, 0.2]
+    q, qd = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0], [0.8, -0.5, 0.3, -1.2, 0.4, 0.9, -0.7]
+    ref = O.integrate(u_prev.unsqueeze(0) + noise, torch.tensor(x + q, dtype=torch.float32),
+                      torch.tensor(vx + qd, dtype=torch.float32), 0.01)
+    e = _engine(model="wholebody", n_samples=K, n_horizon=H, noise="injected", sigma=sigma.numpy())
+    e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    e.set_u_prev(u_prev.numpy())
+    state = np.array(x + [0.0, 0.0, 0.0, 1.0] + q + vx + qd, np.float64)
+    e.step(state, noise.numpy()[None])
+    pos = e.get_trajectory()[0][..., :10]
+    assert np.isfinite(pos).all()
+    _close(pos, ref.numpy(), atol=2e-5, rtol=2e-6, what="positions")
