@@ -11,9 +11,10 @@
 //
 // Lane mapping: a wave64 holds R = 64/L rollouts, one
 // L-lane segment each, lane = timestep t (L = pow2 >= H, 16..64; H > 64 runs
-// ceil(H/64) chunks per lane).  The two cumsums of the integrator are DPP
-// segment scans in fp64 (torch's CPU cumsum accumulates in double); the FK
-// chain, cost and softmin are lane-local; S_k is a segment reduction.
+// ceil(H/64) chunks per lane).  The two cumsums of the integrator run in a
+// transposed lane map through the wave's LDS slot (integrate_lds; DPP segment scans
+// for H > 64); the FK chain, cost and softmin are lane-local; S_k is a segment
+// reduction.
 // Trajectories are stored as SoA planes (V,C,K,H): every store instruction of a
 // wave writes 64 consecutive floats (256 B).
 #pragma once
