@@ -154,6 +154,14 @@ class Engine:
         self._out = np.zeros((self.V, self.out_dim), np.float64)
         self._u0 = np.zeros((self.V, self.A), np.float32)
         self._stats = (capi.Stats * self.V)()
+        # persistent host buffers with their ctypes pointers made once: ndarray.ctypes.data_as
+        # costs ~3-4 us per call, several of them per control call (the latency path)
+        self._state_buf = np.zeros((self.V, self.state_dim), np.float64)
+        self._tgt_pos = np.zeros(3, np.float32)
+        self._tgt_quat = np.zeros(4, np.float32)
+        self._p_out, self._p_u0 = capi.dptr(self._out), capi.fptr(self._u0)
+        self._p_state = capi.dptr(self._state_buf)
+        self._p_tpos, self._p_tquat = capi.fptr(self._tgt_pos), capi.fptr(self._tgt_quat)
 
     # ------------------------------------------------------------------ admin
     def close(self):
@@ -189,9 +197,11 @@ class Engine:
         capi.check(self._L.mppi_set_stream(self._h, C.c_void_p(stream_handle)), "set_stream")
 
     def set_target(self, pos, quat=None, vehicle: int = 0):
-        p = np.ascontiguousarray(pos, np.float32).reshape(3)
-        q = None if quat is None else np.ascontiguousarray(quat, np.float32).reshape(4)
-        capi.check(self._L.mppi_set_target(self._h, vehicle, capi.fptr(p), capi.fptr(q)), "set_target")
+        self._tgt_pos[:] = np.reshape(pos, 3)
+        if quat is not None:
+            self._tgt_quat[:] = np.reshape(quat, 4)
+        capi.check(self._L.mppi_set_target(self._h, vehicle, self._p_tpos,
+                                           None if quat is None else self._p_tquat), "set_target")
 
     def set_joint_trajectory(self, traj=None, vehicle: int = 0):
         """Joint tracking target (H, nq) of the joint_track cost term (None = zeros)."""
@@ -208,8 +218,8 @@ class Engine:
         return u
 
     def set_state(self, state):
-        s = np.ascontiguousarray(state, np.float64).reshape(self.V, self.state_dim)
-        capi.check(self._L.mppi_set_state(self._h, capi.dptr(s)), "set_state")
+        self._state_buf[...] = np.reshape(state, (self.V, self.state_dim))
+        capi.check(self._L.mppi_set_state(self._h, self._p_state), "set_state")
 
     def set_step_counter(self, step: int):
         capi.check(self._L.mppi_set_step_counter(self._h, step & 0xFFFFFFFF), "set_step_counter")
@@ -217,11 +227,14 @@ class Engine:
     # ------------------------------------------------------------------- step
     def step(self, state=None, noise=None):
         """One control step: returns (out (V,out_dim) float64, u0 (V,A), [StepStats])."""
-        s = None if state is None else np.ascontiguousarray(state, np.float64).reshape(self.V, self.state_dim)
+        ps = None
+        if state is not None:
+            self._state_buf[...] = np.reshape(state, (self.V, self.state_dim))
+            ps = self._p_state
         n = None if noise is None else np.ascontiguousarray(noise, np.float32).reshape(
             self.V, self.K, self.H, self.A)
-        capi.check(self._L.mppi_step(self._h, capi.dptr(s), capi.fptr(n), capi.dptr(self._out),
-                                     capi.fptr(self._u0), self._stats), "mppi_step")
+        capi.check(self._L.mppi_step(self._h, ps, capi.fptr(n), self._p_out, self._p_u0, self._stats),
+                   "mppi_step")
         return self._out.copy(), self._u0.copy(), self.stats()
 
     def rollout(self, d_noise_ptr: int = 0):
@@ -231,8 +244,7 @@ class Engine:
         capi.check(self._L.mppi_finalize(self._h), "finalize")
 
     def read_outputs(self):
-        capi.check(self._L.mppi_read_outputs(self._h, capi.dptr(self._out), capi.fptr(self._u0),
-                                             self._stats), "read_outputs")
+        capi.check(self._L.mppi_read_outputs(self._h, self._p_out, self._p_u0, self._stats), "read_outputs")
         return self._out.copy(), self._u0.copy(), self.stats()
 
     def run_steps(self, n: int):
