@@ -418,6 +418,15 @@ constexpr int wave_slot_floats() {
                                                                      : 4 + NCH * 64 * NA;
 }
 
+// Hand-off between lanes of one wave through LDS: a wave's LDS instructions execute in
+// order, so no s_waitcnt is needed; the wavefront-scope fences order the accesses in the
+// memory model and keep the compiler from moving them (rocPRIM's wave_barrier idiom).
+__device__ __forceinline__ void wave_lds_handoff() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int CTRL>
 __device__ __forceinline__ float row_shr_f32(float x) {   // out-of-row sources read 0
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
@@ -431,7 +440,7 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     constexpr int P = G::P, CPS = G::CPS, CL = G::CL, S = G::S;
 #pragma unroll
     for (int a = 0; a < NA; ++a) xw[lane * P + a] = act[a];
-    asm volatile("" ::: "memory");   // a wave's LDS ops execute in order: no wait needed
+    wave_lds_handoff();
     const int sr = lane / CPS, ch = lane & (CPS - 1);
     const bool on = sr < S;
     const int seg = sr / NA, a = sr - seg * NA;
@@ -457,12 +466,12 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     const float v0 = on ? vel0f[a] : 0.0f;
     const float q0 = fmaf((float)(ch * CL) * dt, v0, Qx);   // chunk start incl. the q0dot drift
     const float vb = dt * (Vx + v0);
-    asm volatile("" ::: "memory");
+    wave_lds_handoff();
     if (on) {
 #pragma unroll
         for (int i = 0; i < CL; ++i) xw[rb + i * P] = fmaf((float)(i + 1), vb, q0 + loc[i]);
     }
-    asm volatile("" ::: "memory");
+    wave_lds_handoff();
 #pragma unroll
     for (int a2 = 0; a2 < NA; ++a2) inc[a2] = xw[lane * P + a2];
 }
