@@ -495,3 +495,13 @@ def test_wholebody_integrator_lane_maps(H):
     pos = e.get_trajectory()[0][..., :10]
     assert np.isfinite(pos).all()
     _close(pos, ref.numpy(), atol=2e-5, rtol=2e-6, what="positions")
+
+
+def test_trajectory_above_4gib_rejected_at_create():
+    """The rollout kernels address one vehicle's trajectory planes through a buffer
+    resource (32-bit offsets): a larger trajectory is refused before any allocation."""
+    from quadrotor_manipulator_mppi_amd import _capi as capi
+    with pytest.raises(capi.MPPIError, match="4 GiB"):
+        _engine(model="wholebody", n_samples=1 << 20, n_horizon=256)
+    e = _engine(model="wholebody", n_samples=1 << 20, n_horizon=256, store_trajectory=False)
+    e.close()
