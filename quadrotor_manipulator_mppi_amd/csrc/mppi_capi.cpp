@@ -712,12 +712,16 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     const int P = (kHdr + e->A * H + 3) & ~3;
     // the rollout kernels address one vehicle's trajectory planes through a buffer
     // resource (32-bit byte offsets) and the record bodies with 32-bit indices
-    if ((c.store_trajectory && (uint64_t)e->C * e->K * H * sizeof(float) > 0xFFFFFFFFull) ||
-        (uint64_t)e->V * e->A * nb * H >= 0x80000000ull) {
+    if (c.store_trajectory && (uint64_t)e->C * e->K * H * sizeof(float) > 0xFFFFFFFFull) {
         const int C = e->C, K = e->K;
         delete e;
         return fail(MPPI_ERR_INVALID_ARG, "trajectory of one vehicle (C=%d x K=%d x H=%d floats) exceeds 4 GiB: "
                     "disable store_trajectory or shard the samples", C, K, H);
+    }
+    if ((uint64_t)e->V * e->A * nb * H >= 0x80000000ull) {
+        const int V = e->V;
+        delete e;
+        return fail(MPPI_ERR_INVALID_ARG, "record bodies (V=%d x A x %d blocks x H=%d) exceed 2^31 floats", V, nb, H);
     }
 
     if (savgol_taps(c.savgol_window, c.savgol_order, e->sg_taps) != 0) {
