@@ -270,8 +270,12 @@ mppi_status mppi_get_timing(mppi_engine* e, double* rollout_ms_total, double* fi
 /* Average device time of the two kernels measured back to back: n rollout launches
  * bracketed by one event pair, then n finalize launches bracketed by another (the
  * per-launch pairs of mppi_enable_timing add ~2-3 us of event overhead each).  The
- * warm start and step counter are saved and restored, so the controller state is
- * unchanged.  Single-shard engines with device noise. */
+ * warm start and step counter are saved and restored, and the timing launches write
+ * their outputs (out/u0/stats, weighted noise) to device scratch, so the controller
+ * state and a pending mppi_read_outputs / mppi_get_weighted_noise are unchanged.  The
+ * trajectory and cost buffers (mppi_get_trajectory / mppi_get_costs / mppi_get_weights)
+ * DO hold the timing loop's last rollout afterwards.  Single-shard engines with device
+ * noise. */
 mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us);
 
 /* Algorithmic HBM bytes one mppi_rollout launch moves. */

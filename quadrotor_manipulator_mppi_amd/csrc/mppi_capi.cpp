@@ -306,6 +306,8 @@ struct mppi_engine {
     float* d_noise_in = nullptr;
     uint32_t step_ctr = 0;              // Philox counter word; +1 per finalized step
     uint32_t out_seq = 0;               // completion-flag value of the step read_outputs waits for
+    uint32_t seq_ctr = 0;               // last completion-flag value handed out: monotonic and
+                                        // independent of step_ctr (mppi_set_step_counter rewinds that)
     bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
@@ -313,7 +315,7 @@ struct mppi_engine {
     float* d_hdr = nullptr;     // (V,nb,4) block record headers
     float* d_rdata = nullptr;   // (V,A,nb,H) block record bodies
     int fin_ts = 1, fin_tsz = 8;   // finalize t-slices
-    unsigned char* d_out = nullptr;   // out doubles | u0 floats | stats floats
+    unsigned char* d_out = nullptr;   // device scratch in h_out's layout (mppi_kernel_timing's outputs)
     float* d_wraw = nullptr;
     float* d_wsmooth = nullptr;
     float* d_w = nullptr;
@@ -719,9 +721,10 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
                     "disable store_trajectory or shard the samples", C, K, H);
     }
     if ((uint64_t)e->V * e->A * nb * H >= 0x80000000ull) {
-        const int V = e->V;
+        const int V = e->V, A = e->A;
         delete e;
-        return fail(MPPI_ERR_INVALID_ARG, "record bodies (V=%d x A x %d blocks x H=%d) exceed 2^31 floats", V, nb, H);
+        return fail(MPPI_ERR_INVALID_ARG, "record bodies (V=%d x A=%d x %d blocks x H=%d = %llu floats) exceed 2^31",
+                    V, A, nb, H, (unsigned long long)V * A * nb * H);
     }
 
     if (savgol_taps(c.savgol_window, c.savgol_order, e->sg_taps) != 0) {
@@ -1106,9 +1109,12 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     if (use_device(e)) return MPPI_ERR_HIP;
     FinParams f = e->fp;
     f.mode = 0;
-    f.seq = e->step_ctr + 1u;   // never 0 (the flags start zeroed) unless the counter wraps
-    if (f.seq == 0u) f.seq = 1u;
-    if (!record_out) f.seq = 0u;   // no completion flag (and no fence) for unread steps
+    f.seq = 0u;   // no completion flag (and no fence) for unread steps
+    if (record_out) {   // a fresh value per read step, never 0 (the flags start zeroed): the flags
+                        // the previous read step left can never satisfy this step's wait
+        f.seq = ++e->seq_ctr;
+        if (f.seq == 0u) f.seq = ++e->seq_ctr;
+    }
     if (sharded(e)) {   // slots [shard][v][P]: header then N[a][t]
         const int64_t P = e->dp.P;
         f.nrec = e->cfg.shard_count;
@@ -1277,6 +1283,15 @@ mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, do
     f.mode = 0;
     f.seq = 0u;   // the throughput path's finalize (no completion flag)
     block_records(e, f);
+    // the timing loop's outputs go to device scratch (same layout as the mapped host
+    // buffer), so a pending read_outputs / get_weighted_noise still returns the last
+    // real step; u_prev is restored below (the trajectory and S are overwritten)
+    f.out = (double*)e->d_out;
+    f.u0 = (float*)(e->d_out + off_u0(e));
+    f.stats = (float*)(e->d_out + off_stats(e));
+    f.flags = (uint32_t*)(e->d_out + off_flags(e));
+    f.wraw = nullptr;
+    f.wsmooth = nullptr;
     float ms0 = 0.0f, ms1 = 0.0f;
     int rc = 0;
 #define KT_TRY(expr)                                                                        \

@@ -30,6 +30,10 @@
 #ifndef MPPI_ROLL_OCC
 #define MPPI_ROLL_OCC 4
 #endif
+// park eps in LDS across the FK and cost (k_rollout, NA >= 7)
+#ifndef MPPI_EPS_STASH
+#define MPPI_EPS_STASH 1
+#endif
 
 namespace {
 
@@ -75,7 +79,9 @@ __device__ __forceinline__ void box_muller32(uint32_t w, float& z0, float& z1) {
     if (MPPI_KO & 32) { z0 = __uint_as_float((w & 0x3FFFFFu) | 0x3F800000u); z1 = z0 - 1.5f; return; }
     const float u1 = ((float)(w >> 14) + 0.5f) * 3.814697265625e-6f;      // 2^-18
     const float u2 = ((float)(w & 0x3FFFu) + 0.5f) * 6.103515625e-5f;     // 2^-14
-    const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+    // -2 ln u1 lies in [1.3e-6, 26.3] (u1 >= 2^-19): the bare v_sqrt_f32 (1 ulp) needs none
+    // of the denormal scaling and correction steps __builtin_sqrtf adds (~12 VALU)
+    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
     z0 = r * __builtin_amdgcn_cosf(u2);
     z1 = r * __builtin_amdgcn_sinf(u2);
 }
@@ -530,11 +536,12 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
     if (tid == 0) rmin_bits = 0x7F800000u;   // +inf
     // touch every kernel-argument line the hot phases read (one s_load per 64 B): they
     // land in the scalar cache while the first group's Philox draw runs below
-    float kwarm = 0.0f;
+    // (an integer fold: uniform, so SALU -- a float sum took one VALU op per line)
+    uint32_t kwarm = 0u;
     {
-        const float* kp = (const float*)&pk;
+        const uint32_t* kp = (const uint32_t*)&pk;
 #pragma unroll
-        for (int o = 0; o < (int)(offsetof(DevParams, sigma) / 4); o += 16) kwarm += kp[o];
+        for (int o = 0; o < (int)(offsetof(DevParams, sigma) / 4); o += 16) kwarm ^= kp[o];
     }
     STAMPW(9);
     // the first group's standard normals overlap the loads above
@@ -622,7 +629,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                 } else {
                     draw_normals<NA>(z, kg, (uint32_t)t, (uint32_t)v, step_ctr, seed_lo, seed_hi);
                 }
-                if (p.sigma_diag) {
+                if (!XC || p.sigma_diag) {   // a full Sigma runs in the extended (XC) kernel
 #pragma unroll
                     for (int a = 0; a < NA; ++a) eps[c][a] = z[a] * sdiag[a];
                 } else {
@@ -635,10 +642,16 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                     }
                 }
             }
+            // the warm-start row first, unconditionally (tc is clamped): inside the select the
+            // compiler turned every LDS read into its own exec-masked branch and s_waitcnt,
+            // NA serial LDS round trips per lane
+            float ur[NA];
+#pragma unroll
+            for (int a = 0; a < NA; ++a) ur[a] = u_lds[tc * NA + a];
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 eps[c][a] = val ? eps[c][a] : 0.0f;
-                act[c][a] = val ? u_lds[tc * NA + a] + eps[c][a] : 0.0f;
+                act[c][a] = val ? ur[a] + eps[c][a] : 0.0f;
             }
             if (p.store_noise && val) {
                 float* dst = p.noise_out + (((size_t)v * K + k) * H + t) * NA;
@@ -652,7 +665,8 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
         float ecov = 0.0f, eact = 0.0f, gts[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) gts[c] = 0.0f;
-        if (XC) {
+        if (XC && p.cost_terms) {   // (the XC kernel also runs a full Sigma without extra terms:
+                                    //  gamma_t / sinv exist only with cost_terms)
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 const int t = t0 + 64 * c;
@@ -746,6 +760,20 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
             }
         }
         if (it == 0) STAMP(3);
+
+        // eps is read again only by the softmin accumulate at the end of the group: park
+        // it in this wave's LDS slot (the integrator is done with it; each lane its own
+        // row, so no hand-off) across the FK and cost, the kernel's register peak.  The
+        // compiler barriers stop it from forwarding the stored values in registers.
+        constexpr bool kStash = MPPI_EPS_STASH && NA >= 7;
+        constexpr int kESP = (NCH == 1) ? IntegGeom<LSEG, NA>::P : NA;   // row pitch (odd for NCH == 1)
+        if constexpr (kStash) {
+#pragma unroll
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) xw[(c * 64 + lane) * kESP + a] = eps[c][a];
+            asm volatile("" ::: "memory");
+        }
 
         // ---- A4-A10: FK + per-step cost, trajectory planes
         float xs[NCH];
@@ -924,6 +952,13 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
             eta_w = eta_w * f + es;
             eta2_w = eta2_w * f * f + e2;
             const float e_mine = (kval && !(S_mine != S_mine)) ? __expf(p.coef * (S_mine - rn)) : 0.0f;
+            if constexpr (kStash) {
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                    for (int a = 0; a < NA; ++a) eps[c][a] = xw[(c * 64 + lane) * kESP + a];
+            }
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -1016,12 +1051,13 @@ inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
-// the extra CostManager terms get their own instantiation: their registers would
-// otherwise be reserved (and spilled) in the common pose-cost-only kernel
+// The extended (XC) instantiation carries the extra CostManager terms and a full
+// (non-diagonal) Sigma: their registers would otherwise be reserved in the common
+// kernel (the full zSigma product alone held the A*A Sigma in VGPRs and forced spills
+// at a 5-wave budget).  The common kernel assumes a diagonal Sigma and no extra terms.
 template <int MODEL, int NA, int NCH, int LSEG, bool F64>
 inline int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
-    if constexpr (MODEL != MPPI_MODEL_DRONE)
-        if (p.cost_terms) return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, true>(p, threads, s);
+    if (p.cost_terms || !p.sigma_diag) return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, true>(p, threads, s);
     return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, false>(p, threads, s);
 }
 
