@@ -291,8 +291,12 @@ int32_t mppi_savgol_coefficients(int32_t window, int32_t order, float* c); /* sv
 mppi_status mppi_host_fk(const mppi_joint* joints, int32_t n_joints, const double* q, const double* xyzquat,
                          int32_t f64, float* T16);
 
-/* Device RNG check: standard normals z (K,H,A) and raw Philox words (K,H,4*ceil(A/4))
- * exactly as the rollout kernel draws them for (seed, step, vehicle, global k0..k0+K). */
+/* Device RNG check: standard normals z (K,H,A) and the raw Philox words (K,H,W),
+ * W = mppi_philox_words(A), exactly as the rollout kernel draws them for (seed, step,
+ * vehicle, global k0..k0+K): A/8 Philox4x32-10 calls, then the A mod 8 remainder from one
+ * Philox2x32-10 call (remainder <= 4) or one more Philox4x32-10 call.
+ * A in {2, 3, 4, 7, 8, 10}. */
+int32_t mppi_philox_words(int32_t A);
 mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, int64_t k0, int32_t K,
                                 int32_t H, int32_t A, int32_t device, float* z, uint32_t* raw);
 

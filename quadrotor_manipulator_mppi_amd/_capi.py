@@ -122,6 +122,7 @@ PROTOTYPES = {
     "mppi_dyn_rnea": (_ST, [_P, _D, _D, _D, _D]),
     "mppi_dyn_terms": (_ST, [_P, _D, _D, _D, _D]),
     "mppi_computed_torque": (_ST, [_P, _D, _D, _D, C.c_double, C.c_double, C.c_int32, _D]),
+    "mppi_philox_words": (C.c_int32, [C.c_int32]),
     "mppi_philox_normals": (_ST, [C.c_uint64, C.c_uint32, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                   C.c_int32, C.c_int32, _F, _U32]),
 }
@@ -153,7 +154,12 @@ def lib():
         except ImportError:
             pass
         h = C.CDLL(LIB_PATH)
+        # MPPI_CAPI_LENIENT=1: tolerate entry points an older build lacks (same-box A/B of
+        # library builds in tools/ only; the shipped binding requires every one)
+        lenient = os.environ.get("MPPI_CAPI_LENIENT") == "1"
         for name, (res, args) in PROTOTYPES.items():
+            if lenient and not hasattr(h, name):
+                continue
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

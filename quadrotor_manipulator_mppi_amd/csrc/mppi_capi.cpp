@@ -1416,20 +1416,38 @@ mppi_status mppi_get_timing(mppi_engine* e, double* rms, double* fms, int64_t* r
     return MPPI_OK;
 }
 
+// Diagnostic (MPPI_STAMPS builds; not part of the public header): the raw per-wave stamps
+// of the last rollout launch, kStamps uint64 per wave.  Returns the wave count (0 when the
+// engine has no stamps) or a negative status.
+int64_t mppi_debug_stamps(mppi_engine* e, unsigned long long* out, int64_t max_waves) {
+    if (!e || !out) return MPPI_ERR_INVALID_ARG;
+    if (!e->d_stamps) return 0;
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const int64_t nwaves = std::min<int64_t>(max_waves, (int64_t)e->V * e->dp.nb * (e->threads / 64));
+    if (hipStreamSynchronize(e->stream) != hipSuccess ||
+        hipMemcpy(out, e->d_stamps, (size_t)nwaves * kStamps * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return MPPI_ERR_HIP;
+    return nwaves;
+}
+
+int32_t mppi_philox_words(int32_t A) {
+    return A < 1 ? 0 : 4 * (A / 8) + ((A % 8) == 0 ? 0 : (A % 8) <= 4 ? 2 : 4);
+}
+
 mppi_status mppi_philox_normals(uint64_t seed, uint32_t step, int32_t vehicle, int64_t k0, int32_t K, int32_t H,
                                 int32_t A, int32_t device, float* z, uint32_t* raw) {
     if (K < 1 || H < 1 || A < 1 || A > MPPI_MAX_ACTION || !z || !raw)
         return fail(MPPI_ERR_INVALID_ARG, "mppi_philox_normals: bad arguments");
     HIP_TRY(hipSetDevice(device));
     const size_t n = (size_t)K * H;
-    const int nj = (A + 7) / 8;   // Philox calls per (k, t): 8 normals each
+    const int nw = mppi_philox_words(A);   // raw Philox words per (k, t)
     float* dz = nullptr;
     uint32_t* dr = nullptr;
     HIP_TRY(hipMalloc(&dz, n * A * sizeof(float)));
-    HIP_TRY(hipMalloc(&dr, n * nj * 4 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dr, n * nw * sizeof(uint32_t)));
     int rc = mppi_launch_philox(seed, step, vehicle, k0, K, H, A, dz, dr, nullptr);
     hipError_t e1 = hipMemcpy(z, dz, n * A * sizeof(float), hipMemcpyDeviceToHost);
-    hipError_t e2 = hipMemcpy(raw, dr, n * nj * 4 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    hipError_t e2 = hipMemcpy(raw, dr, n * nw * sizeof(uint32_t), hipMemcpyDeviceToHost);
     (void)hipFree(dz);
     (void)hipFree(dr);
     if (rc) return fail(MPPI_ERR_HIP, "philox launch failed (%d)", rc);

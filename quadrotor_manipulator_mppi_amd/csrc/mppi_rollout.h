@@ -30,6 +30,10 @@
 #ifndef MPPI_ROLL_OCC
 #define MPPI_ROLL_OCC 4
 #endif
+// wave priority by remaining rollout groups (k_rollout, iters > 1)
+#ifndef MPPI_PRIO
+#define MPPI_PRIO 1
+#endif
 // park eps in LDS across the FK and cost (k_rollout, NA >= 7)
 #ifndef MPPI_EPS_STASH
 #define MPPI_EPS_STASH 1
@@ -64,6 +68,14 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
     }
 }
 
+// s_setprio takes an immediate: min(r, 3) for a wave-uniform r
+__device__ __forceinline__ void set_wave_prio(int r) {
+    if (r >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (r == 2) __builtin_amdgcn_s_setprio(2);
+    else if (r == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 __device__ __forceinline__ float uniform_f32(float x) {   // wave-uniform value kept in an SGPR
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
@@ -86,13 +98,40 @@ __device__ __forceinline__ void box_muller32(uint32_t w, float& z0, float& z1) {
     z1 = r * __builtin_amdgcn_sinf(u2);
 }
 
-// z[a] for a < NA: Philox call j (counter (kg, t, veh<<8 | j, step)) gives normals
-// 8j .. 8j+7, word i of it the pair (8j+2i, 8j+2i+1).
+// Philox2x32-10 (Salmon et al., SC'11; Random123's philox2x32): one 32x32 -> 64 multiply
+// per round instead of two, for the draws that need at most 2 words.
+__device__ __forceinline__ void philox2x10(uint32_t& c0, uint32_t& c1, uint32_t k) {
+    k = __builtin_amdgcn_readfirstlane(k);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(k) :: "scc");
+        const uint64_t p = (uint64_t)0xD256D193u * c0;   // one v_mad_u64_u32
+        const uint32_t n0 = xor3_sk((uint32_t)(p >> 32), c1, k);
+        c1 = (uint32_t)p;
+        c0 = n0;
+    }
+}
+
+// The key of the Philox2x32 draws: the 64-bit seed folded to 32 bits, plus the control
+// step times the golden ratio (a bijection of the step for a fixed seed).
+__host__ __device__ __forceinline__ uint32_t philox2_key(uint32_t seed_lo, uint32_t seed_hi, uint32_t step) {
+    return (seed_lo ^ (seed_hi * 0x85EBCA6Bu)) + step * 0x9E3779B9u;
+}
+
+// Standard normals z[a], a < NA, of sample kg at step t (noise):
+//   * normals 8j .. 8j+7 (j < NA/8): Philox4x32-10 call j, counter (kg, t, veh<<8 | j, step),
+//     key (seed lo, seed hi); word i gives the pair (8j+2i, 8j+2i+1);
+//   * the r = NA mod 8 left over: r <= 4 -> one Philox2x32-10 call, counter
+//     (kg, veh<<8 | t), key philox2_key(seed, step), its words giving pairs 8J.., 8J+2..
+//     (J = NA/8); r >= 5 -> Philox4x32-10 call J as above.
+// (the whole-body's 10 dims: one 4x32 call + one 2x32 call, 30 multiplies instead of 40)
 template <int NA>
 __device__ __forceinline__ void draw_normals(float (&z)[NA], uint32_t kg, uint32_t t, uint32_t veh,
                                              uint32_t step, uint32_t s0, uint32_t s1) {
+    constexpr int J = NA / 8, REM = NA % 8;
+    constexpr int N4 = J + (REM >= 5 ? 1 : 0);   // Philox4x32 calls
 #pragma unroll
-    for (int j = 0; j < (NA + 7) / 8; ++j) {
+    for (int j = 0; j < N4; ++j) {
         uint32_t w[4] = {kg, t, (veh << 8) | (uint32_t)j, step};
         if (!(MPPI_KO & 2)) philox10(w[0], w[1], w[2], w[3], s0, s1);
 #pragma unroll
@@ -104,6 +143,23 @@ __device__ __forceinline__ void draw_normals(float (&z)[NA], uint32_t kg, uint32
             if (8 * j + 2 * i + 1 < NA) z[8 * j + 2 * i + 1] = b;
         }
     }
+    if constexpr (REM >= 1 && REM <= 4) {
+        uint32_t w[2] = {kg, (veh << 8) | t};
+        if (!(MPPI_KO & 2)) philox2x10(w[0], w[1], philox2_key(s0, s1, step));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (8 * J + 2 * i >= NA) break;
+            float a, b;
+            box_muller32(w[i], a, b);
+            z[8 * J + 2 * i] = a;
+            if (8 * J + 2 * i + 1 < NA) z[8 * J + 2 * i + 1] = b;
+        }
+    }
+}
+
+// Philox words one (k, t) draw consumes (the raw layout of k_philox / oracle.philox_normals)
+__host__ __device__ constexpr int philox_words(int NA) {
+    return 4 * (NA / 8) + ((NA % 8) == 0 ? 0 : (NA % 8) <= 4 ? 2 : 4);
 }
 
 // ---------------------------------------------------------------- FK helpers
@@ -317,9 +373,24 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                \
         STAMP(i);                                                                  \
     } while (0)
+// STAMPRT: the 100 MHz real-time counter (s_memrealtime), slots 13/14 = wave start/end:
+// wall-clock wave lifetimes, the shader clock (memtime / realtime) and the grid's timeline
+#define STAMPRT(i)                                                                                    \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        if (pk.stamps && lane == 0) {                                                                 \
+            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
+            if ((i) == 13) /* where the wave ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4) */        \
+                pk.stamps[w_ * kStamps + 15] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
+                                               (unsigned)__builtin_amdgcn_s_getreg(0xF804);           \
+        }                                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
 #else
 #define STAMP(i) do { } while (0)
 #define STAMPW(i) do { } while (0)
+#define STAMPRT(i) do { } while (0)
 #endif
 
 // Inclusive fp32 segment sum (cost reduction; order-insensitive at tolerance).
@@ -508,6 +579,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;   // block size as a preloaded argument: blockDim would be an implicit-argument s_load
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
+    STAMPRT(13);
     STAMP(0);
     // issue the global loads first (addresses need only preloaded scalars and the
     // kernarg pointer), keep the values in registers across the Philox draw
@@ -810,7 +882,8 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                 }
                 if (MPPI_KO & 4) {
                     T.m[3] += posf[c][QOFF]; T.m[7] += posf[c][QOFF + 1];
-                } else if (NQ == 7 && p.chain_fast == 2) {   // Kinova: origin rotations are signed permutations
+                } else if (NQ == 7 && (!XC || p.chain_fast == 2)) {   // Kinova: origin rotations are signed
+                    // permutations (the common kernel runs only this chain; any other goes to XC)
                     kin_joint<0>(T, jnt[p.j0 + 0].O, qang(c, 0));
                     kin_joint<1>(T, jnt[p.j0 + 1].O, qang(c, 1));
                     kin_joint<2>(T, jnt[p.j0 + 2].O, qang(c, 2));
@@ -818,6 +891,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
                     kin_joint<4>(T, jnt[p.j0 + 4].O, qang(c, 4));
                     kin_joint<5>(T, jnt[p.j0 + 5].O, qang(c, 5));
                     kin_joint<6>(T, jnt[p.j0 + 6].O, qang(c, 6));
+                } else if (!XC) {   // (unreachable: the common kernel is dispatched for Kinova chains only)
                 } else if (p.chain_fast) {   // nq revolute-z joints, q_index = 0..nq-1 in order
 #pragma unroll
                     for (int j = 0; j < NQ; ++j) {
@@ -969,7 +1043,15 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
     if (p.iters == 1) {
         group(0);
     } else {
-        for (int it = 0; it < p.iters; ++it) group(it);
+        // Wave priority by remaining groups: the SIMD arbiter otherwise favours the oldest
+        // wave, so the waves of a SIMD finish their (equal) work one after another and the
+        // last ones run alone, without latency hiding (the grid's tail).  A
+        // wave that is ahead drops its priority, the laggards catch up.
+        for (int it = 0; it < p.iters; ++it) {
+            if (MPPI_PRIO) set_wave_prio(p.iters - 1 - it);
+            group(it);
+        }
+        if (MPPI_PRIO) set_wave_prio(0);
     }
     STAMP(5);
 
@@ -1032,6 +1114,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
         p.rdata[rbase + (uint32_t)a * rstride + (uint32_t)t] = s;
     }
     STAMP(7);
+    STAMPRT(14);
 }
 
 // =============================================================================
@@ -1051,13 +1134,18 @@ inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
-// The extended (XC) instantiation carries the extra CostManager terms and a full
-// (non-diagonal) Sigma: their registers would otherwise be reserved in the common
-// kernel (the full zSigma product alone held the A*A Sigma in VGPRs and forced spills
-// at a 5-wave budget).  The common kernel assumes a diagonal Sigma and no extra terms.
+// The extended (XC) instantiation carries the extra CostManager terms, a full
+// (non-diagonal) Sigma and the generic FK chains: their registers would otherwise be
+// reserved in the common kernel (the full zSigma product alone held the A*A Sigma in
+// VGPRs; with the generic chain loops the whole-body kernel needed 98 VGPRs, without
+// them 87).  The common kernel assumes a diagonal Sigma, no extra terms and the Kinova
+// chain (or no chain: the drone).
 template <int MODEL, int NA, int NCH, int LSEG, bool F64>
 inline int launch_rollout_t(const DevParams& p, int threads, hipStream_t s) {
-    if (p.cost_terms || !p.sigma_diag) return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, true>(p, threads, s);
+    const bool generic_chain = MODEL != MPPI_MODEL_DRONE && !(NA - (MODEL == MPPI_MODEL_WHOLEBODY ? 3 : 0) == 7 &&
+                                                              p.chain_fast == 2);
+    if (p.cost_terms || !p.sigma_diag || generic_chain)
+        return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, true>(p, threads, s);
     return launch_rollout_x<MODEL, NA, NCH, LSEG, F64, false>(p, threads, s);
 }
 

@@ -317,7 +317,7 @@ class Engine:
 def philox_normals(seed: int, step: int, vehicle: int, k0: int, K: int, H: int, A: int, device: int = 0):
     L = capi.lib()
     z = np.empty((K, H, A), np.float32)
-    raw = np.empty((K, H, 4 * ((A + 7) // 8)), np.uint32)   # one Philox call per 8 normals
+    raw = np.empty((K, H, L.mppi_philox_words(A)), np.uint32)   # the words in consumption order
     capi.check(L.mppi_philox_normals(seed, step, vehicle, k0, K, H, A, device, capi.fptr(z),
                                      raw.ctypes.data_as(C.POINTER(C.c_uint32))), "philox_normals")
     return raw, z

@@ -25,6 +25,12 @@ Fixture map:
   arm_k64_h32_allcosts.npz F7 arm MPPI with every CostManager term the reference
                               ships disabled (cost_manager.py:83-87) switched on,
                               fp64 state near a joint limit, 2 steps
+  arm_k32_h32_gap.npz     F2c arm MPPI with the sampler's Sigma at 1.0 I (10x the
+                              default 0.1 I of standard_normal_noise.py:17), so the
+                              top-2 cost gap is >= 20 lambda in both steps: the arm
+                              path end to end at the plain 1e-4 rel bar, 2 steps
+
+Regenerate one fixture only:  python tests/golden/make_golden.py --only arm_k32_h32_gap
 """
 import contextlib
 import io
@@ -157,10 +163,12 @@ def _enable_all_costs(cm, rec_terms):
     cm.compute_all_cost = compute_all_cost
 
 
-def make_arm(path, K, H, steps, f64, seed0, state, all_costs=False):
+def make_arm(path, K, H, steps, f64, seed0, state, all_costs=False, sigma_scale=None):
     with _quiet():
         m = ArmMPPI()
     _resize_arm(m, K, H)
+    if sigma_scale is not None:   # the sampler's own Sigma attribute (standard_normal_noise.py:17)
+        m.sample_gen.sigma = torch.eye(m.n_action) * sigma_scale
     terms = {}
     if all_costs:
         _enable_all_costs(m.cost_manager, terms)
@@ -172,7 +180,8 @@ def make_arm(path, K, H, steps, f64, seed0, state, all_costs=False):
     out = {"K": K, "H": H, "A": 7, "dt": m.dt, "lam": m._lambda, "state_f64": int(f64),
            "q_full": np.array(q_full, np.float64), "v_full": np.array(v_full, np.float64),
            "target_pos": np.array(ARM_TARGET_POS, np.float32),
-           "target_quat": np.array(ARM_TARGET_QUAT, np.float32), "steps": steps}
+           "target_quat": np.array(ARM_TARGET_QUAT, np.float32), "steps": steps,
+           "sigma": _np(m.sample_gen.sigma)}
     gaps = []
     for s in range(steps):
         m.update_joint(q_full, v_full)
@@ -387,6 +396,10 @@ def make_wholebody(path, K, H, steps, seed0):
 def main():
     torch.set_num_threads(1)
     d = HERE
+    if "--only" in sys.argv:
+        only = sys.argv[sys.argv.index("--only") + 1]
+        FIXTURES[only](d)
+        return
     make_drone(os.path.join(d, "drone_k128_h20.npz"), 128, 20, 3, 100, [0.0, 0.0, 1.0], [0.0, 0.0, 0.0])
     make_drone(os.path.join(d, "drone_k256_h32.npz"), 256, 32, 2, 200, [0.2, -0.1, 1.5], [0.1, 0.0, -0.2])
     c3 = ([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0], HOME_Q, [0.0] * 6, [0.0] * 7)
@@ -404,6 +417,14 @@ def main():
                   [1.57, 1.7, 0.0, 4.4, 0.0, 5.1485, 0.0],         # joint 6 2e-4 under its 5.1487 limit
                   [0.0] * 6, [0.0, 0.3, 0.0, -0.2, 0.0, 0.0, 0.0])
     make_arm(os.path.join(d, "arm_k64_h32_allcosts.npz"), 64, 32, 2, True, 700, near_limit, all_costs=True)
+    FIXTURES["arm_k32_h32_gap"](d)
+
+
+FIXTURES = {
+    "arm_k32_h32_gap": lambda d: make_arm(
+        os.path.join(d, "arm_k32_h32_gap.npz"), 32, 32, 2, True, 800,
+        ([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0], HOME_Q, [0.0] * 6, [0.0] * 7), sigma_scale=1.0),
+}
 
 
 if __name__ == "__main__":

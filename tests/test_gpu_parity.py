@@ -49,7 +49,7 @@ def _amplified_bound(dS_max, w, noise, lam):
 def test_device_philox_matches_restatement():
     from quadrotor_manipulator_mppi_amd.engine import philox_normals
     for (seed, step, veh, k0, K, H, A) in [(1234, 0, 0, 0, 64, 32, 7), (2**40 + 7, 5, 3, 4096, 32, 64, 10),
-                                           (99, 1, 0, 7, 16, 20, 3)]:
+                                           (99, 1, 0, 7, 16, 20, 3), (5, 2, 2, 100, 8, 24, 4)]:
         raw, z = philox_normals(seed, step, veh, k0, K, H, A)
         raw_ref, z_ref = O.philox_normals(seed, step, veh, np.arange(k0, k0 + K), H, A)
         assert np.array_equal(raw, raw_ref), "Philox words must be bit-exact"
@@ -122,6 +122,35 @@ def test_arm_matches_reference_fixture(name, terms):
         _close(u0[0], u0_ref, atol=float(sm_bound.max()) + 1e-6, what="u0")
         _close(out[0, 7:], vdes_ref, atol=u0_tol * dt + 1e-7, what="vdes")
         _close(out[0, :7], qdes_ref, atol=u0_tol * dt * dt + 1e-7, what="qdes")
+        assert st[0].reach == bool(g[f"s{s}_reach"])
+
+
+def test_arm_matches_reference_fixture_plain_tolerance():
+    """F2c: the arm fixture whose top-2 cost gap is >= 20 lambda in both steps (the
+    sampler's Sigma at 1.0 I), so the whole arm step -- w, w_eps, SavGol, u_prev,
+    qdes, vdes -- meets the north star's plain 1e-4 rel against the reference, with
+    no conditioning bound (mppi.py:122-169)."""
+    g = load_golden("arm_k32_h32_gap.npz")
+    K, H = int(g["K"]), int(g["H"])
+    assert np.all(g["top2_gap"] >= 20 * 0.1)
+    e = _engine(model="arm", n_samples=K, n_horizon=H, noise="injected", state_f64=True,
+                sigma=g["sigma"])
+    e.set_target(g["target_pos"], g["target_quat"])
+    state = np.concatenate([g["q_full"][:7], g["q_full"][7:], g["v_full"][6:]])
+    for s in range(int(g["steps"])):
+        e.set_u_prev(g[f"s{s}_u_prev_in"])
+        out, u0, st = e.step(state, g[f"s{s}_noise"][None])
+        tr = e.get_trajectory()[0]
+        _close(tr[..., :7], g[f"s{s}_q_samples"], atol=2e-6, what="q_samples")
+        _close(tr[..., 7:], g[f"s{s}_ee"].reshape(K, H, 16), atol=2e-5, what="EE")
+        _close(e.get_costs()[0], g[f"s{s}_S"], rtol=2e-5, what="S")
+        _close(e.get_weights()[0], g[f"s{s}_w"], rtol=1e-4, atol=1e-12, what="w")
+        raw, sm = e.get_weighted_noise()
+        _close(raw[0], g[f"s{s}_w_eps_raw"], rtol=1e-4, atol=1e-6, what="w_eps raw")
+        _close(sm[0], g[f"s{s}_w_eps"], rtol=1e-4, atol=1e-6, what="w_eps savgol")
+        _close(e.get_u_prev()[0], g[f"s{s}_u_prev_out"], rtol=1e-4, atol=1e-6, what="u_prev")
+        _close(out[0, :7], g[f"s{s}_qdes"], rtol=1e-6, atol=1e-9, what="qdes")
+        _close(out[0, 7:], g[f"s{s}_vdes"], rtol=1e-4, atol=1e-9, what="vdes")
         assert st[0].reach == bool(g[f"s{s}_reach"])
 
 

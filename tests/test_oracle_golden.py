@@ -93,7 +93,8 @@ def test_drone_noise_reproduces_reference_randn():
     _eq(eps.numpy(), g["s0_noise"])
 
 
-@pytest.mark.parametrize("name", ["arm_k32_h32_f32.npz", "arm_k32_h32_f64.npz", "arm_k100_h32_f64.npz"])
+@pytest.mark.parametrize("name", ["arm_k32_h32_f32.npz", "arm_k32_h32_f64.npz", "arm_k100_h32_f64.npz",
+                                  "arm_k32_h32_gap.npz"])
 def test_arm_steps(kinova_chain, name):
     g = load_golden(name)
     f64 = bool(g["state_f64"])
@@ -131,6 +132,16 @@ def test_arm_noise_reproduces_reference_randn():
     g = load_golden("arm_k32_h32_f32.npz")
     torch.manual_seed(300)
     _eq(O.draw_noise(32, 32, torch.eye(7) * 0.1).numpy(), g["s0_noise"])
+    g = load_golden("arm_k32_h32_gap.npz")    # the sampler's Sigma set to 1.0 I
+    torch.manual_seed(800)
+    _eq(O.draw_noise(32, 32, torch.from_numpy(g["sigma"])).numpy(), g["s0_noise"])
+
+
+def test_gap_fixture_is_well_conditioned():
+    """F2c exists so the arm path meets the plain 1e-4 rel bar end to end: its
+    top-2 cost gap must be >= 20 lambda in every step."""
+    g = load_golden("arm_k32_h32_gap.npz")
+    assert np.all(g["top2_gap"] >= 20 * 0.1)
 
 
 def test_wholebody_steps(kinova_chain):
@@ -167,13 +178,34 @@ def test_philox_known_answer():
     assert [int(x) for x in out] == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
 
 
+def test_philox2x32_known_answer():
+    """Random123 known-answer vectors for philox2x32-10 (the remainder draw)."""
+    assert [int(x) for x in O.philox2x32_10(0, 0, 0)] == [0xff1dae59, 0x6cd10df2]
+    assert [int(x) for x in O.philox2x32_10(0xffffffff, 0xffffffff, 0xffffffff)] == [0x2c3f628b, 0xab4fd7ad]
+    assert [int(x) for x in O.philox2x32_10(0x243f6a88, 0x85a308d3, 0x13198a2e)] == [0xdd7ce038, 0xf62a4c12]
+
+
+def test_philox_streams_are_distinct():
+    """The remainder draw's key changes with the step (a bijection for a fixed seed) and
+    its counter with (k, t, vehicle): no two (k, t, vehicle, step) of a control run
+    share the Philox2x32 input."""
+    keys = {O.philox2_key(0x5EED, s) for s in range(4096)}
+    assert len(keys) == 4096
+    raw0, _ = O.philox_normals(7, 0, 0, np.arange(64), 32, 10)
+    raw1, _ = O.philox_normals(7, 1, 0, np.arange(64), 32, 10)
+    raw2, _ = O.philox_normals(7, 0, 1, np.arange(64), 32, 10)
+    assert raw0.shape == (64, 32, 6)
+    for other in (raw1, raw2):
+        assert not np.any(raw0[..., 4] == other[..., 4]) or np.mean(raw0[..., 4] == other[..., 4]) < 1e-3
+
+
 def test_philox_normals_moments():
     """The device mapping (one Box-Muller pair per Philox word, 18-bit radius, 14-bit
     angle): per-dim moments, a KS test on 2e5 draws, no cross-dim correlation."""
     from scipy import stats
-    for A in (4, 7, 10):
+    for A in (3, 4, 7, 10):
         raw, z = O.philox_normals(1234, 0, 0, np.arange(2048), 32, A)
-        assert raw.shape == (2048, 32, 4 * ((A + 7) // 8))
+        assert raw.shape == (2048, 32, O.philox_words(A))
         z = z.astype(np.float64).reshape(-1, A)
         assert np.all(np.abs(z.mean(0)) < 0.01) and np.all(np.abs(z.std(0) - 1.0) < 0.01)
         c = np.corrcoef(z.T) - np.eye(A)
