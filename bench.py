@@ -1,18 +1,25 @@
 #!/usr/bin/env python3
 """MPPI control-step benchmark (BASELINE.json metric: rollout-steps/s, K x H
-state-steps, plus control-step p50 latency, at K=4096 H=32).
+state-steps, plus control-step p50 latency).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload arm_c3]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+    python bench.py [--gpus 1] [--steps K] [--warmup W] [--workload arm_c3]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N ...
 
 A "step" is one MPPI control step (noise -> rollout -> FK -> cost -> softmin ->
 SavGol -> update) over one batch of synthetic state/goal input.
-Scaling is WEAK: every rank owns K samples of the same controller (sample
-sharding, one all-reduce per step), so the whole-job rate is N*K*H per step.
-``value`` is measured with state and warm start resident on the GPU (async
-steps, one sync at the end); the host-inclusive call latency (H2D state, D2H
-outputs, check_reach) is reported separately as latency_p50/p99.
+
+Workloads:
+* plain ``python bench.py`` (N=1): ``arm_c3`` -- the configuration BASELINE.json's
+  metric is quoted on (Kinova arm, K=4096 H=32, configs[2]); ``scaling`` "weak".
+* under torch.distributed.run (WORLD_SIZE set, any N): ``c4`` -- the north star,
+  whole-body K=65536 H=64 (configs[3]) with the samples split 65536/N per rank (strong
+  scaling at the fixed K), one RCCL all-reduce per step; ``scaling`` "strong".  The N=1
+  line of that curve is also in every plain N=1 run as ``secondary.c4``.
+``value`` is the whole job's rollout-steps per second with state and warm start resident
+on the GPU (back-to-back steps, one host sync), bracketed by barrier + synchronize on
+both sides and the max over ranks.  The host-inclusive call latency (state H2D, outputs,
+check_reach) is ``latency_p50/p99_ms`` (never ``value``).
 
 Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
 """
@@ -21,6 +28,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -33,6 +41,7 @@ HOME_Q = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]                # kinova.py:135
 ARM_TARGET = ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])   # mppi.py:71-72
 DRONE_TARGET = [1.0, 2.0, 3.4]                                   # drone_mppi.py:141
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+C4_K_TOTAL = 65536      # BASELINE configs[3]: whole-body K=65536 H=64 over the node
 
 WORKLOADS = {
     # configs[2]: Kinova arm MPPI with on-GPU FK chain, K=4096 H=32 (BASELINE metric shape)
@@ -41,20 +50,43 @@ WORKLOADS = {
     # configs[1]: drone MPPI K=4096 H=32
     "drone_c2": dict(model="drone", n_samples=4096, n_horizon=32,
                      desc="Drone MPPI K=4096 H=32 (BASELINE configs[1])"),
-    # configs[3] per-GPU shard: whole-body K=65536 H=64 over 8 GPUs -> 8192 per GPU
+    # configs[3], the north star: whole-body K=65536 H=64, samples split over the ranks
+    "c4": dict(model="wholebody", n_samples=C4_K_TOTAL, n_horizon=64, strong=True,
+               desc="Whole-body MPPI K=65536 H=64, samples split K/N per GPU (BASELINE configs[3])"),
+    # configs[3] per-GPU shard at N=8: whole-body 8192 samples H=64 on one GPU
     "wholebody_c4": dict(model="wholebody", n_samples=8192, n_horizon=64,
-                         desc="Whole-body MPPI, 8192 samples/GPU H=64 (BASELINE configs[3] shard)"),
-    # configs[4] per-GPU share: 64 vehicles x K=8192 over 8 GPUs -> 8 vehicles per GPU
+                         desc="Whole-body MPPI, 8192 samples/GPU H=64 (BASELINE configs[3] shard at N=8)"),
     # the 6-DoF rigid-body quadrotor (commented out in the reference), drone sizes
     "quadrotor_c2": dict(model="quadrotor", n_samples=4096, n_horizon=32,
                          desc="6-DoF quadrotor MPPI K=4096 H=32 (SURVEY §8f rank 3; configs[1] sizes)"),
+    # configs[4] per-GPU share: 64 vehicles x K=8192 over 8 GPUs -> 8 vehicles per GPU
     "fleet_c5": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=8,
                      desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
 }
 
+# the CPU baseline's shapes (C4 K-reduced: the full C4 on CPU is impractical)
+CPU_SHAPES = {
+    "c1_drone_k128_h20": ("drone", 128, 20),
+    "c2_drone_k4096_h32": ("drone", 4096, 32),
+    "c3_arm_k4096_h32": ("arm", 4096, 32),
+    "c4r_wholebody_k4096_h64": ("wholebody", 4096, 64),
+}
+CPU_HEADLINE = {"arm_c3": "c3_arm_k4096_h32", "drone_c2": "c2_drone_k4096_h32",
+                "wholebody_c4": "c4r_wholebody_k4096_h64", "c4": "c4r_wholebody_k4096_h64",
+                "fleet_c5": "c4r_wholebody_k4096_h64"}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def build_info():
+    """The library build this run loaded (written by quadrotor_manipulator_mppi_amd/build.py)."""
+    try:
+        with open(os.path.join(ROOT, "quadrotor_manipulator_mppi_amd", "lib", "BUILD_INFO.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
 
 
 def make_state(model: str, V: int) -> np.ndarray:
@@ -67,7 +99,7 @@ def make_state(model: str, V: int) -> np.ndarray:
             rows.append([0.0, 0.0, 1.0, 0.0, 0.0, 0.0] + [0.0] * 6)
         elif model == "arm":
             rows.append([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0] + HOME_Q + [0.0] * 7)
-        else:
+        else:   # vehicle v > 0 offset by U(-0.5,0.5) m xyz, U(-0.2,0.2) rad joints
             off = rng.uniform(-0.5, 0.5, 3) if v else np.zeros(3)
             joff = rng.uniform(-0.2, 0.2, 7) if v else np.zeros(7)
             rows.append(list(np.array([0.0, 0.0, 1.0]) + off) + [0.0, 0.0, 0.0, 1.0]
@@ -80,82 +112,123 @@ def set_targets(eng, model, V):
     for v in range(V):
         if model in ("drone", "quadrotor"):
             eng.set_target(DRONE_TARGET, vehicle=v)
-        else:
+        else:   # targets jittered by +-0.1 m for v > 0
             p = np.array(ARM_TARGET[0]) + (rng.uniform(-0.1, 0.1, 3) if v else 0.0)
             eng.set_target(p, ARM_TARGET[1], vehicle=v)
 
 
 def load_traffic(workload: str):
-    """Per-launch HBM bytes of the rollout kernel from the committed rocprofv3
-    PMC summary (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), if present."""
+    """Per-launch HBM bytes of the rollout kernel from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) and where it came from."""
     path = os.path.join(ROOT, "profiles", "pmc_rollout.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
+    w = d.get(workload, {})
+    src = (f"profiles/pmc_rollout.json[{workload}]: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+           f"separate passes, avg per k_rollout launch; collected on build {w.get('build_head', '?')}")
+    return w.get("hbm_bytes_per_launch"), src if w else None
 
 
-def cpu_baseline(workload: str, budget_s: float):
-    """The oracle (op-for-op torch-CPU restatement of the reference step, randn
-    included) timed on the host cores on a bounded sample of the same workload."""
+# ------------------------------------------------------------------------------ CPU baseline
+def _cpu_step_fn(model: str, K: int, H: int):
+    """One control step of the oracle (op-for-op torch-CPU restatement of the reference's
+    compute_control_input, randn included) at a shape with the reference's C1-C4 inputs."""
     import torch
     from oracle import mppi_oracle as O
     from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain
-    w = WORKLOADS[workload]
-    K, H, model = w["n_samples"], w["n_horizon"], w["model"]
-    threads = torch.get_num_threads()
-    times = []
+    chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
     if model == "quadrotor":
         sig = torch.diag(torch.tensor([30.0, 1.0, 1.0, 1.0]))
         u = torch.zeros(H, 4)
         u[:, 0] = 14.7 * 9.81
-
-        def one():
-            return O.quad_step([0, 0, 1.0, 0, 0, 0], [0.0] * 6, u, O.draw_noise(K, H, sig), DRONE_TARGET)
-    elif model == "drone":
+        return lambda: O.quad_step([0, 0, 1.0, 0, 0, 0], [0.0] * 6, u, O.draw_noise(K, H, sig), DRONE_TARGET)
+    if model == "drone":
         sig = torch.eye(3) * 30.0
         u = torch.zeros(H, 3)
-
-        def one():
-            return O.drone_step([0, 0, 1.0], [0, 0, 0.0], u, O.draw_noise(K, H, sig), DRONE_TARGET)
-    elif model == "arm":
-        chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
+        return lambda: O.drone_step([0, 0, 1.0], [0, 0, 0.0], u, O.draw_noise(K, H, sig), DRONE_TARGET)
+    if model == "arm":
         sig = torch.eye(7) * 0.1
         u = torch.zeros(H, 7)
         qf = np.array([0, 0, 1.0, 0, 0, 0, 1] + HOME_Q)
         vf = np.zeros(13)
-
-        def one():
-            return O.arm_step(chain, qf, vf, u, O.draw_noise(K, H, sig), *ARM_TARGET, f64=True)
-    else:
-        chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
-        sig = torch.diag(torch.tensor([30.0] * 3 + [0.1] * 7))
-        u = torch.zeros(H, 10)
-        rpy = O.base_rpy_from_quat([0, 0, 0, 1.0])
-
-        def one():
-            return O.wholebody_step(chain, [0, 0, 1.0], [0, 0, 0.0], HOME_Q, [0.0] * 7, rpy, u,
+        return lambda: O.arm_step(chain, qf, vf, u, O.draw_noise(K, H, sig), *ARM_TARGET, f64=True)
+    sig = torch.diag(torch.tensor([30.0] * 3 + [0.1] * 7))
+    u = torch.zeros(H, 10)
+    rpy = O.base_rpy_from_quat([0, 0, 0, 1.0])
+    return lambda: O.wholebody_step(chain, [0, 0, 1.0], [0, 0, 0.0], HOME_Q, [0.0] * 7, rpy, u,
                                     O.draw_noise(K, H, sig), *ARM_TARGET)
-    one()   # warm-up
+
+
+def _time_cell(fn, budget_s: float, min_steps: int = 3, warmup: int = 2):
+    for _ in range(warmup):
+        fn()
+    times = []
     t_end = time.perf_counter() + budget_s
-    while time.perf_counter() < t_end or len(times) < 3:
+    while time.perf_counter() < t_end or len(times) < min_steps:
         t0 = time.perf_counter()
-        one()
+        fn()
         times.append(time.perf_counter() - t0)
-    p50 = float(np.median(times))
-    return {"value": K * H / p50, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
-            "p50_ms": p50 * 1e3,
-            "sample": f"{len(times)} oracle control steps (torch-CPU restatement of the reference, randn "
-                      f"included) at {workload} K={K} H={H}, {threads} threads, median"}
+    return np.array(times)
 
 
-def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=True):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(workload: str, cell_budget_s: float):
+    """the oracle's control step (randn included) at C1, C2, C3 and a
+    K-reduced C4, with torch's full thread pool (the job's share of the host cores) and
+    with one thread, p50 and p99.  The headline is the cell of this run's workload."""
+    import torch
+    n_all = torch.get_num_threads()
+    cells = {}
+    for name, (model, K, H) in CPU_SHAPES.items():
+        fn = _cpu_step_fn(model, K, H)
+        cells[name] = {"model": model, "K": K, "H": H}
+        for tag, nt in (("threads_all", n_all), ("threads_1", 1)):
+            torch.set_num_threads(nt)
+            t = _time_cell(fn, cell_budget_s)
+            p50, p99 = float(np.median(t)), float(np.percentile(t, 99))
+            cells[name][tag] = {"threads": nt, "steps": int(t.size), "p50_ms": p50 * 1e3, "p99_ms": p99 * 1e3,
+                                "rollout_steps_per_s": K * H / p50}
+            log(f"cpu {name} {tag}={nt}: p50 {p50 * 1e3:.2f} ms p99 {p99 * 1e3:.2f} ms ({t.size} steps)")
+        torch.set_num_threads(n_all)
+    head = cells[CPU_HEADLINE.get(workload, "c3_arm_k4096_h32")]
+    host = {"os_cpu_count": os.cpu_count(), "cpu_model": cpu_model(), "torch_threads": n_all,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    hv = head["threads_all"]
+    line = {"value": hv["rollout_steps_per_s"], "unit": "rollout-steps/s", "cores": n_all, "kind": "port",
+            "p50_ms": hv["p50_ms"], "p99_ms": hv["p99_ms"],
+            "value_1thread": head["threads_1"]["rollout_steps_per_s"],
+            "sample": (f"{hv['steps']} oracle control steps (torch-CPU op-for-op restatement of the reference, "
+                       f"randn included) at {head['model']} K={head['K']} H={head['H']}, {n_all} threads "
+                       f"(os.cpu_count()={host['os_cpu_count']}, {host['cpu_model']}), median; "
+                       f"{cell_budget_s:.1f} s per cell, all cells in cpu_baseline_all"),
+            "host": host}
+    return line, cells
+
+
+# ------------------------------------------------------------------------------ GPU runs
+def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
     import torch
     from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
     w = dict(WORKLOADS[name])
     w.pop("desc")
+    strong = w.pop("strong", False)
+    if strong:
+        if w["n_samples"] % world:
+            raise SystemExit(f"{name}: K={w['n_samples']} does not split over {world} ranks")
+        w["n_samples"] //= world
     V = w.get("n_vehicles", 1)
     native = None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False
     se = ShardedEngine(seed=1234, native=native, **w)
@@ -173,42 +246,39 @@ def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=Tru
             dist.barrier()
         torch.cuda.synchronize()
 
-    def steps(n):
-        # one C call enqueues n control steps (rollout -> all-reduce over the engine's
-        # RCCL communicator -> finalize when sharded); the gloo rehearsal path loops in Python
-        se.run_steps(n)
-
-    steps(warmup)
+    se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
+    eng.synchronize()
     barrier()
     t0 = time.perf_counter()
-    steps(steps_n)
+    se.run_steps(steps_n)
     eng.synchronize()
     barrier()
     dt = time.perf_counter() - t0
     tim = None
     if timing:   # per-kernel HIP-event timing in its own region (events perturb the step rate)
-        n_t = max(50, steps_n // 2)
-        if world == 1:   # n launches of each kernel back to back between one event pair; the
-            # median of 5 such batches (a transient clock dip on the box moves one batch, not the median)
-            nb_ = max(50, n_t // 5)
-            rs, fs = zip(*[eng.kernel_timing(nb_) for _ in range(5)])
-            r_us, f_us = float(np.median(rs)), float(np.median(fs))
-            tim = {"rollout_us": r_us, "finalize_us": f_us,
-                   "method": f"HIP events around {nb_} back-to-back launches, median of 5 batches",
-                   "rollout_us_batches": [round(x, 3) for x in rs]}
-        else:            # sharded engines: an event pair around every launch (~2-3 us overhead each)
-            eng.enable_timing(True)
-            steps(n_t)
+        n_t = max(50, steps_n // 5)
+        # n launches of each kernel back to back between one event pair, then n (rollout,
+        # finalize) pairs as a step runs them; median of 5 batches (a transient clock dip on
+        # the box moves one batch, not the median)
+        rs, fs, ps = zip(*[eng.kernel_timing_ex(n_t) for _ in range(5)])
+        r_us, f_us, p_us = float(np.median(rs)), float(np.median(fs)), float(np.median(ps))
+        tim = {"rollout_us": r_us, "finalize_us": f_us, "pair_us": p_us,
+               "rollout_in_step_us": max(r_us, p_us - f_us),
+               "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
+                         f"median of 5 batches, on the engine stream",
+               "rollout_us_batches": [round(x, 3) for x in rs]}
+        if se.native and world > 1:   # the step's one collective alone (collective call on every rank)
+            tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
+            se.run_steps(1)   # repack the slots the timing loop summed in place
             eng.synchronize()
-            t = eng.timing()
-            eng.enable_timing(False)
-            tim = {"rollout_us": 1e3 * t["rollout_ms_total"] / max(1, t["n_rollout"]),
-                   "finalize_us": 1e3 * t["finalize_ms_total"] / max(1, t["n_finalize"]),
-                   "method": "HIP event pair per launch"}
     if dist is not None:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        if tim is not None:   # the slowest rank's kernels
+            r = torch.tensor([tim["rollout_us"], tim["rollout_in_step_us"]], device="cuda", dtype=torch.float64)
+            dist.all_reduce(r, op=dist.ReduceOp.MAX)
+            tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = map(float, r.tolist())
     # host-inclusive control-call latency (set_state H2D + step + D2H outputs + check_reach)
     lat = []
     for i in range(lat_steps + 20):
@@ -219,10 +289,22 @@ def run_workload(name, steps_n, warmup, rank, world, dist, lat_steps, timing=Tru
     out, u0, st = eng.read_outputs()
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
-    res = {"dt": dt, "tim": tim, "lat": lat, "K": eng.K, "H": eng.H, "A": eng.A, "V": V,
-           "bytes": eng.rollout_bytes(), "ess": float(st[0].ess), "cfg": eng.cfg}
+    res = {"dt": dt, "tim": tim, "lat": lat, "K": eng.K, "H": eng.H, "A": eng.A, "V": V, "strong": strong,
+           "bytes": eng.rollout_bytes(), "ess": float(st[0].ess), "cfg": eng.cfg, "native": se.native,
+           "nranks": world}
     eng.close()
     return res
+
+
+def roofline_of(r):
+    tim = r["tim"]
+    us = tim["rollout_in_step_us"]
+    achieved = r["bytes"] / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "kernel": "k_rollout_quad" if r["cfg"].model == 3 else "k_rollout",
+            "bytes_per_launch": r["bytes"], "kernel_us": us,
+            "kernel_us_basis": "rollout in a control step: (rollout+finalize pair) - finalize, >= back-to-back",
+            "frac_back_to_back": r["bytes"] / (tim["rollout_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
 
 
 def main():
@@ -230,17 +312,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--workload", default="arm_c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: arm_c3 for a plain run, c4 (north star, strong scaling) under torchrun")
     ap.add_argument("--latency-steps", type=int, default=200)
-    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--cpu-budget", type=float, default=2.5, help="seconds of CPU sampling per baseline cell")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,quadrotor_c2",
+    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
 
     import torch
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    workload = args.workload or ("c4" if launched else "arm_c3")
     # ranks beyond the visible devices wrap (rehearsing N ranks on fewer GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = None
@@ -258,56 +343,65 @@ def main():
     from quadrotor_manipulator_mppi_amd import _capi
     _capi.lib()
 
-    r = run_workload(args.workload, args.steps, args.warmup, rank, world, dist, args.latency_steps)
+    r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps)
     K, H, V = r["K"], r["H"], r["V"]
     per_step = r["dt"] / args.steps
     value = world * V * K * H / per_step
     tim = r["tim"]
-    avg_roll_ms = tim["rollout_us"] * 1e-3
-    avg_fin_ms = tim["finalize_us"] * 1e-3
-    achieved = r["bytes"] / (avg_roll_ms * 1e-3) / 1e9
     lat = np.array(r["lat"]) * 1e3
     secondary = {}
     if world == 1 and args.secondary:
-        for wname in [s for s in args.secondary.split(",") if s]:
-            s = run_workload(wname, max(50, args.steps // 5), 20, rank, world, dist, 50)
-            st = s["tim"]
-            ms = st["rollout_us"] * 1e-3
+        for wname in [s for s in args.secondary.split(",") if s and s != workload]:
+            ns = max(50, args.steps // 5)
+            s = run_workload(wname, ns, 20, 1, None, 50)
+            rf = roofline_of(s)
             secondary[wname] = {
-                "value": s["V"] * s["K"] * s["H"] / (s["dt"] / max(50, args.steps // 5)),
-                "ms_per_step": 1e3 * s["dt"] / max(50, args.steps // 5),
+                "value": s["V"] * s["K"] * s["H"] / (s["dt"] / ns), "ms_per_step": 1e3 * s["dt"] / ns,
                 "latency_p50_ms": float(np.median(np.array(s["lat"]) * 1e3)) if s["lat"] else None,
-                "rollout_kernel_us": ms * 1e3,
-                "rollout_GBps": s["bytes"] / (ms * 1e-3) / 1e9,
-                "roofline_frac": s["bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                "samples": s["K"], "horizon": s["H"], "vehicles": s["V"],
+                "rollout_kernel_us": rf["kernel_us"], "rollout_back_to_back_us": s["tim"]["rollout_us"],
+                "finalize_us": s["tim"]["finalize_us"], "rollout_GBps": rf["achieved"],
+                "roofline_frac": rf["frac"], "roofline_frac_back_to_back": rf["frac_back_to_back"]}
             log(f"secondary {wname}: {secondary[wname]}")
-    cpu = None
+    cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.workload, args.cpu_budget)
+        cpu, cpu_all = cpu_baseline(workload, args.cpu_budget)
         log(f"cpu baseline: {cpu}")
     if rank == 0:
-        traffic = load_traffic(args.workload)
+        traffic, traffic_src = load_traffic(workload)
+        rf = roofline_of(r)
+        rf.update({"traffic": traffic, "traffic_source": traffic_src})
+        desc = WORKLOADS[workload]["desc"]
         line = {
             "metric": "MPPI rollouts/sec (K x H state-steps) + control-step p50 latency, K=4096 H=32",
             "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (reference C3 state/goal: home joints, base at (0,0,1), mppi.py target)",
-            "config": {"workload": args.workload, "desc": WORKLOADS[args.workload]["desc"],
-                       "samples_per_gpu": K, "horizon": H, "action_dim": r["A"], "vehicles_per_gpu": V,
-                       "noise": "device Philox4x32-10", "state_dtype": "f64" if r["cfg"].state_f64 else "f32",
-                       "parallelism": f"samples-sharded x{world}, 1 all-reduce/step" if world > 1 else "1 GPU"},
+            "scaling": "strong" if r["strong"] else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (reference state/goal: home joints, base at (0,0,1), mppi.py / drone_mppi.py targets; "
+                    "device Philox noise)",
+            "config": {"workload": workload, "desc": desc, "samples_total": world * K * V if not r["strong"]
+                       else WORKLOADS[workload]["n_samples"], "samples_per_gpu": K, "horizon": H,
+                       "action_dim": r["A"], "vehicles_per_gpu": V, "noise": "device Philox4x32-10 (+2x32)",
+                       "state_dtype": "f64" if r["cfg"].state_f64 else "f32",
+                       "parallelism": (f"samples sharded over {world} GPUs, 1 all-reduce/step" if world > 1
+                                       else "1 GPU")},
             "latency_p50_ms": float(np.median(lat)) if lat.size else None,
             "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
-            "kernels": {"rollout_us": avg_roll_ms * 1e3, "finalize_us": avg_fin_ms * 1e3,
-                        "timing": tim["method"]},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout_quad" if r["cfg"].model == 3 else "k_rollout",
-                         "bytes_per_launch": r["bytes"]},
+            "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"},
+            "roofline": rf,
             "cpu_baseline": cpu,
+            "cpu_baseline_all": cpu_all,
             "secondary": secondary or None,
+            "build": build_info(),
         }
+        if world > 1:
+            line["multi_gpu"] = {
+                "rccl_nranks": r["nranks"], "collective": (
+                    "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
+                    if r["native"] else "torch.distributed all_reduce(SUM) of the slots"),
+                "allreduce_us": tim.get("allreduce_us"),
+                "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks"),
+                "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -278,6 +278,18 @@ mppi_status mppi_get_timing(mppi_engine* e, double* rollout_ms_total, double* fi
  * noise. */
 mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us);
 
+/* mppi_kernel_timing plus pair_us: the average of n (rollout, finalize) pairs launched as
+ * a control step runs them (the rollout after a finalize, its inputs just written).  Also
+ * on a shard: the finalize then combines the exchange slots as they stand (no collective).
+ * pair_us may be NULL. */
+mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us,
+                                  double* pair_us);
+
+/* Average time of the step's all-reduce (mppi_exchange) over n back-to-back calls on the
+ * engine stream.  Collective: every rank of the communicator calls it with the same n.
+ * The slots are summed in place, so run a step (which repacks them) before reading outputs. */
+mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us);
+
 /* Algorithmic HBM bytes one mppi_rollout launch moves. */
 int64_t mppi_rollout_bytes(const mppi_config* cfg);
 

@@ -110,6 +110,8 @@ PROTOTYPES = {
     "mppi_enable_timing": (_ST, [_P, C.c_int32]),
     "mppi_get_timing": (_ST, [_P, _D, _D, _I64, _I64]),
     "mppi_kernel_timing": (_ST, [_P, C.c_int32, _D, _D]),
+    "mppi_kernel_timing_ex": (_ST, [_P, C.c_int32, _D, _D, _D]),
+    "mppi_exchange_timing": (_ST, [_P, C.c_int32, _D]),
     "mppi_rollout_bytes": (C.c_int64, [_CFG]),
     "mppi_joint_origin": (None, [C.POINTER(Joint), _F]),
     "mppi_base_transform": (None, [_D, C.c_int32, _F]),

@@ -80,7 +80,31 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False, stamp
     if res.returncode != 0:
         raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, out)
+    _write_build_info(out)
     return out
+
+
+def _write_build_info(out: str) -> None:
+    """lib/BUILD_INFO.json: which source state a library came from (bench.py reports it;
+    the GPU box has no .git)."""
+    import datetime
+    import json
+    head = None
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no", "--",
+                                "quadrotor_manipulator_mppi_amd/csrc", "include"], capture_output=True, text=True,
+                               timeout=10).stdout.strip()
+        if head and dirty:
+            head += "+dirty"
+    except (OSError, subprocess.SubprocessError):
+        pass
+    info = {"library": os.path.basename(out), "git_head": head, "arch": ARCH, "extra_flags": EXTRA,
+            "built_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
+    if out == LIB:
+        with open(os.path.join(LIB_DIR, "BUILD_INFO.json"), "w") as f:
+            json.dump(info, f, indent=1)
 
 
 if __name__ == "__main__":
@@ -89,5 +113,5 @@ if __name__ == "__main__":
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic build with per-phase s_memtime stamps")
     a = ap.parse_args()
-    print(build(force=a.force or True, debug=a.debug, verbose=True, stamps=a.stamps))
+    print(build(force=a.force, debug=a.debug, verbose=True, stamps=a.stamps))
     sys.exit(0)

@@ -694,11 +694,13 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     const int nw = e->threads / 64;
     const int groups = (e->K + nw * R - 1) / (nw * R);
     int nb = c.blocks_per_vehicle;
-    // auto: one block per group while the grid is at most 512 blocks (2 per CU at 4 waves
-    // per SIMD); above that >= 2 groups per block (the prologue and the block combine are
-    // amortised, fewer records for the finalize), capped at 1024 blocks in total.
-    // Measured on MI355X (tools/geom_sweep.py, profiles/r01/geom_sweep_s3.txt): WB K=8192
-    // 20.2 us at 512 blocks vs 21.6 at 1024; K=65536 best at 1024; V=8 fleet at 128/vehicle.
+    // auto: one block per group (iters == 1: the single-group kernel) while the grid is at
+    // most 512 blocks (2 per CU); above that >= 2 groups per block (the looping kernel; the
+    // prologue and the block combine are amortised, fewer records for the finalize),
+    // capped at 1024 blocks in total.  Measured on MI355X (tools/geom_sweep.py,
+    // tools/ab_interleave.py): WB K=8192 15.0 us at 512 looping blocks vs
+    // 16.3 at 1024 single-group blocks (8 waves/SIMD) -- whose finalize also reads twice
+    // the records (7.4 vs 5.6 us); K=65536 best at 1024; V=8 fleet at 128/vehicle.
     if (nb <= 0) {
         nb = (groups * e->V <= 512) ? groups : std::min(std::max(1, groups / 2), std::max(1, 1024 / e->V));
     }
@@ -1066,6 +1068,18 @@ static void block_records(const mppi_engine* e, FinParams& f) {
     f.dat = e->d_rdata; f.d_vs = (int64_t)e->A * nb * H; f.d_as = nb * H; f.d_rs = H;
 }
 
+// The finalize's record source: the rollout blocks' records, or the exchange slots of a shard.
+static void final_records(const mppi_engine* e, FinParams& f) {
+    if (sharded(e)) {   // slots [shard][v][P]: header then N[a][t]
+        const int64_t P = e->dp.P;
+        f.nrec = e->cfg.shard_count;
+        f.hdr = e->d_exchange; f.hdr_vs = P; f.hdr_rs = (int64_t)e->V * P;
+        f.dat = e->d_exchange + kHdr; f.d_vs = P; f.d_as = e->H; f.d_rs = (int64_t)e->V * P;
+    } else {
+        block_records(e, f);
+    }
+}
+
 mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_rollout before mppi_set_state");
@@ -1115,14 +1129,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
         f.seq = ++e->seq_ctr;
         if (f.seq == 0u) f.seq = ++e->seq_ctr;
     }
-    if (sharded(e)) {   // slots [shard][v][P]: header then N[a][t]
-        const int64_t P = e->dp.P;
-        f.nrec = e->cfg.shard_count;
-        f.hdr = e->d_exchange; f.hdr_vs = P; f.hdr_rs = (int64_t)e->V * P;
-        f.dat = e->d_exchange + kHdr; f.d_vs = P; f.d_as = e->H; f.d_rs = (int64_t)e->V * P;
-    } else {
-        block_records(e, f);
-    }
+    final_records(e, f);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
     int rc = mppi_launch_finalize(&f, e->stream);
@@ -1266,15 +1273,18 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     return MPPI_OK;
 }
 
-mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
-    if (!e || n <= 0 || !rollout_us || !finalize_us) return fail(MPPI_ERR_INVALID_ARG, "mppi_kernel_timing: bad arguments");
-    if (sharded(e)) return fail(MPPI_ERR_STATE, "mppi_kernel_timing is single-shard");
+mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us,
+                                  double* pair_us) {
+    if (!e || n <= 0 || !rollout_us || !finalize_us)
+        return fail(MPPI_ERR_INVALID_ARG, "mppi_kernel_timing: bad arguments");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_kernel_timing needs device noise");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_kernel_timing before mppi_set_state");
+    if (sharded(e) && !e->d_exchange)
+        return fail(MPPI_ERR_STATE, "mppi_kernel_timing on a shard needs its exchange buffer");
     if (use_device(e)) return MPPI_ERR_HIP;
     const size_t ub = sizeof(float) * e->V * e->H * e->A;
     float* saved = nullptr;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     mppi_status st = MPPI_OK;
     DevParams p = e->dp;
     p.vc0 = e->h_vc[0];
@@ -1282,17 +1292,18 @@ mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, do
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // the throughput path's finalize (no completion flag)
-    block_records(e, f);
+    final_records(e, f);
     // the timing loop's outputs go to device scratch (same layout as the mapped host
     // buffer), so a pending read_outputs / get_weighted_noise still returns the last
-    // real step; u_prev is restored below (the trajectory and S are overwritten)
+    // real step; u_prev is restored below (the trajectory and S are overwritten).  On a
+    // shard the finalize combines the exchange slots as they stand (no collective here).
     f.out = (double*)e->d_out;
     f.u0 = (float*)(e->d_out + off_u0(e));
     f.stats = (float*)(e->d_out + off_stats(e));
     f.flags = (uint32_t*)(e->d_out + off_flags(e));
     f.wraw = nullptr;
     f.wsmooth = nullptr;
-    float ms0 = 0.0f, ms1 = 0.0f;
+    float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
     int rc = 0;
 #define KT_TRY(expr)                                                                        \
     do {                                                                                    \
@@ -1307,17 +1318,53 @@ mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, do
     KT_TRY(hipEventRecord(ev[1], e->stream));
     for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_finalize(&f, e->stream);
     KT_TRY(hipEventRecord(ev[2], e->stream));
+    // the kernels as a control step runs them: rollout after finalize (u_prev and the
+    // records just written, cold in the other XCDs' L2)
+    for (int i = 0; i < n && rc == 0 && pair_us; ++i) {
+        rc = mppi_launch_rollout(&p, e->threads, e->stream);
+        if (rc == 0) rc = mppi_launch_finalize(&f, e->stream);
+    }
+    KT_TRY(hipEventRecord(ev[3], e->stream));
     KT_TRY(hipMemcpyAsync(e->d_u_prev, saved, ub, hipMemcpyDeviceToDevice, e->stream));
     KT_TRY(hipStreamSynchronize(e->stream));
     if (rc != 0) { st = fail(MPPI_ERR_HIP, "kernel launch failed (%d)", rc); goto done; }
     KT_TRY(hipEventElapsedTime(&ms0, ev[0], ev[1]));
     KT_TRY(hipEventElapsedTime(&ms1, ev[1], ev[2]));
+    KT_TRY(hipEventElapsedTime(&ms2, ev[2], ev[3]));
     *rollout_us = 1e3 * ms0 / n;
     *finalize_us = 1e3 * ms1 / n;
+    if (pair_us) *pair_us = 1e3 * ms2 / n;
 #undef KT_TRY
 done:
     for (auto x : ev) if (x) (void)hipEventDestroy(x);
     if (saved) (void)hipFree(saved);
+    return st;
+}
+
+mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
+    return mppi_kernel_timing_ex(e, n, rollout_us, finalize_us, nullptr);
+}
+
+// n back-to-back all-reduces of the exchange slots on the engine stream between one event
+// pair (collective: every rank calls it with the same n).  The slots are summed in place,
+// so the call leaves the exchange buffer scaled by shard_count^n: run a step after it.
+mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us) {
+    if (!e || n <= 0 || !allreduce_us) return fail(MPPI_ERR_INVALID_ARG, "mppi_exchange_timing: bad arguments");
+    if (!e->comm) return fail(MPPI_ERR_STATE, "mppi_exchange_timing needs mppi_comm_init");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    mppi_status st = MPPI_OK;
+    float ms = 0.0f;
+    HIP_TRY(hipEventCreate(&ev[0]));
+    if (hipEventCreate(&ev[1]) != hipSuccess) { (void)hipEventDestroy(ev[0]); return fail(MPPI_ERR_HIP, "hipEventCreate"); }
+    if (hipEventRecord(ev[0], e->stream) != hipSuccess) st = fail(MPPI_ERR_HIP, "hipEventRecord");
+    for (int i = 0; i < n && st == MPPI_OK; ++i) st = mppi_exchange(e);
+    if (st == MPPI_OK && (hipEventRecord(ev[1], e->stream) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
+                          hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess))
+        st = fail(MPPI_ERR_HIP, "exchange timing events failed");
+    if (st == MPPI_OK) *allreduce_us = 1e3 * ms / n;
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
     return st;
 }
 

@@ -557,8 +557,14 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
 // (-mllvm -amdgpu-kernarg-preload-count, build.py): the first group's Philox
 // draw and the u_prev / joint-table loads start without waiting for the
 // kernel-argument segment (its first s_load costs ~1.5k cycles).
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC>
-__global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+// ONEG: every wave runs exactly one rollout group (iters == 1).  Straight-line code with
+// no loop-carried softmin state: the common whole-body kernel fits in 52 VGPRs, so it is
+// budgeted for 8 waves per SIMD (the looping variant needs 87: 5 waves; the fp64-state
+// arm kernel would spill at 64 and keeps the 4-wave budget -- C3 runs 2 waves per SIMD).  At the C4 shard
+// (whole-body K=8192 H=64) that is 1024 blocks x 8 waves, all resident at once: twice the
+// latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
+__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
                                                  const int32_t nthr,
@@ -832,6 +838,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
             }
         }
         if (it == 0) STAMP(3);
+        if (ONEG && MPPI_PRIO) set_wave_prio(2);   // progress priority (single group): see below
 
         // eps is read again only by the softmin accumulate at the end of the group: park
         // it in this wave's LDS slot (the integrator is done with it; each lane its own
@@ -965,6 +972,7 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
             }
         }
         if (it == 0) STAMP(4);
+        if (ONEG && MPPI_PRIO) set_wave_prio(1);
 
         // ---- S_k = fl(ws * sum_{t<H-1} x_t) + fl(wt * x_{H-1}) per segment (wave-uniform picks)
         float st = 0.0f;
@@ -1040,7 +1048,15 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
             rho_w = rn;
         }
     };
-    if (p.iters == 1) {
+    if (ONEG) {
+        // Progress priority: 3 until the integrator is done, 2 through FK and cost, 1 for the
+        // softmin, 0 in the block combine.  The waves of a SIMD start over ~2 us of launch
+        // ramp; under the arbiter's oldest-first order the early ones would finish early and
+        // leave the late ones to run alone -- here a wave that is ahead yields.
+        if (MPPI_PRIO) set_wave_prio(3);
+        group(0);
+        if (MPPI_PRIO) set_wave_prio(0);
+    } else if (p.iters == 1) {
         group(0);
     } else {
         // Wave priority by remaining groups: the SIMD arbiter otherwise favours the oldest
@@ -1120,18 +1136,26 @@ __global__ void __launch_bounds__(512, MPPI_ROLL_OCC) k_rollout(const uint32_t s
 // =============================================================================
 // launchers
 // =============================================================================
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
-inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
+inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>()) * sizeof(float);
     if (p.V == 1)
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>), dim3(p.nb, p.V), dim3(threads), lds,
+                           s, p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
                            p.u_prev, p.joints, p);
     else
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC>), dim3(p.nb, p.V), dim3(threads), lds, s,
-                           p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
+        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>), dim3(p.nb, p.V), dim3(threads), lds,
+                           s, p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
                            p.u_prev, p.joints, p);
     return (int)hipGetLastError();
+}
+
+// the single-group (ONEG) variant exists for the common kernel at NCH == 1
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
+inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
+    if constexpr (!XC && NCH == 1)
+        if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true>(p, threads, s);
+    return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false>(p, threads, s);
 }
 
 // The extended (XC) instantiation carries the extra CostManager terms, a full

@@ -44,6 +44,21 @@ def all_reduce_slots(buf: torch.Tensor, group=None) -> torch.Tensor:
     return buf
 
 
+def share_comm_id(rank: int, world: int, group=None, make_id: Optional[Callable[[], bytes]] = None) -> bytes:
+    """Rank 0 makes the RCCL unique id (``mppi_comm_unique_id``) and every rank receives it
+    over torch.distributed (any backend), as ncclCommInitRank requires.  Raises on a
+    malformed id, so no rank enters the collective init with a bad one."""
+    from . import _capi
+    make_id = make_id or Engine.comm_unique_id
+    uid = [make_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0, group=group)
+    if not isinstance(uid[0], (bytes, bytearray)) or len(uid[0]) != _capi.COMM_ID_BYTES:
+        raise RuntimeError(f"rank {rank}: bad RCCL unique id from rank 0 "
+                           f"({type(uid[0]).__name__}, {len(uid[0]) if uid[0] is not None else 0} bytes)")
+    return bytes(uid[0])
+
+
 def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
     """Host restatement of the finalize combine for a (G, P) slot array -> raw
     w_eps (H, A).  Used by the CPU (gloo) tests of the exchange protocol; the
@@ -79,10 +94,7 @@ class ShardedEngine:
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
         if self.native:   # engine-owned RCCL communicator: the whole step is enqueued from C
-            uid = [Engine.comm_unique_id() if self.rank == 0 else None]
-            if self.world > 1:
-                dist.broadcast_object_list(uid, src=0, group=group)
-            self.engine.comm_init(uid[0])
+            self.engine.comm_init(share_comm_id(self.rank, self.world, group))
         elif self.world > 1:
             slot = self.engine.exchange_slot_floats()
             with torch.cuda.stream(self.stream):

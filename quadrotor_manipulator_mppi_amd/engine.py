@@ -310,6 +310,20 @@ class Engine:
         capi.check(self._L.mppi_kernel_timing(self._h, n, C.byref(r), C.byref(f)), "kernel_timing")
         return r.value, f.value
 
+    def kernel_timing_ex(self, n: int = 200):
+        """(rollout_us, finalize_us, pair_us): back-to-back averages of each kernel, and of
+        (rollout, finalize) pairs as a control step runs them.  Also on a shard."""
+        r, f, pr = C.c_double(), C.c_double(), C.c_double()
+        capi.check(self._L.mppi_kernel_timing_ex(self._h, n, C.byref(r), C.byref(f), C.byref(pr)),
+                   "kernel_timing_ex")
+        return r.value, f.value, pr.value
+
+    def exchange_timing(self, n: int = 100) -> float:
+        """Average all-reduce time (us) of the engine's RCCL communicator (collective)."""
+        us = C.c_double()
+        capi.check(self._L.mppi_exchange_timing(self._h, n, C.byref(us)), "exchange_timing")
+        return us.value
+
     def rollout_bytes(self) -> int:
         return int(self._L.mppi_rollout_bytes(C.byref(self.cfg)))
 

@@ -19,7 +19,7 @@ import torch.multiprocessing as mp
 
 from conftest import load_golden
 from oracle import mppi_oracle as O
-from quadrotor_manipulator_mppi_amd.distributed import HDR, all_reduce_slots, combine_slots
+from quadrotor_manipulator_mppi_amd.distributed import HDR, all_reduce_slots, combine_slots, share_comm_id
 
 
 def _slot_len(A, H):
@@ -125,3 +125,61 @@ def test_gloo_world2_exchange(name, V):
         rho, eta, N = O.shard_partial(torch.as_tensor(S + v), torch.as_tensor(eps), lam)
         want = (N / eta).numpy()
         np.testing.assert_allclose(res[0][2][v], want, rtol=2e-5, atol=1e-6 * np.abs(want).max())
+
+
+# ----------------------------------------------------------- native RCCL path (host side)
+def _uid_rank(rank, world, port, q, bad):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        made = []
+
+        def make_id():
+            made.append(rank)
+            return b"x" * 7 if bad else bytes(range(128))
+        try:
+            q.put((rank, share_comm_id(rank, world, make_id=make_id), made))
+        except RuntimeError as e:
+            q.put((rank, str(e), made))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad", [False, True])
+def test_comm_id_broadcast_world2(bad):
+    """The engine-owned RCCL path's id hand-off (distributed.share_comm_id): only rank 0
+    makes the ncclUniqueId, every rank receives the same 128 bytes over torch.distributed;
+    a malformed id is refused on every rank before ncclCommInitRank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uid_rank, args=(r, world, port, q, bad)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][2] == [0] and res[1][2] == [], "only rank 0 makes the id"
+    if bad:
+        assert all("bad RCCL unique id" in r[1] for r in res)
+    else:
+        assert res[0][1] == res[1][1] == bytes(range(128))
+
+
+def test_native_comm_entry_points_reject_bad_arguments():
+    """mppi_comm_unique_id / mppi_comm_init / mppi_exchange / mppi_exchange_timing check
+    their arguments before touching RCCL or a device (CPU-callable)."""
+    import ctypes as C
+    from quadrotor_manipulator_mppi_amd import _capi as capi
+    L = capi.lib()
+    assert L.mppi_comm_unique_id(None) == capi.ERR_INVALID_ARG
+    buf = (C.c_uint8 * capi.COMM_ID_BYTES)()
+    assert L.mppi_comm_init(None, buf) == capi.ERR_INVALID_ARG
+    assert L.mppi_exchange(None) == capi.ERR_INVALID_ARG
+    us = C.c_double()
+    assert L.mppi_exchange_timing(None, 10, C.byref(us)) == capi.ERR_INVALID_ARG
+    r, f, pr = C.c_double(), C.c_double(), C.c_double()
+    assert L.mppi_kernel_timing_ex(None, 10, C.byref(r), C.byref(f), C.byref(pr)) == capi.ERR_INVALID_ARG
+    assert "bad arguments" in L.mppi_last_error().decode()
