@@ -5,7 +5,7 @@
 tag=${1:-dev}; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/gpu_tests_$tag.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$tag.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/gpu_tests_$tag.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err
