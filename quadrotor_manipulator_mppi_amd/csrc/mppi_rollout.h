@@ -410,9 +410,13 @@ __device__ __forceinline__ float seg_scan_f32(float x) {
 // planes of one vehicle are one buffer resource (C*K*H*4 < 4 GiB, checked at create):
 // the lane's byte offset sits in one VGPR and the plane offset in an SGPR, so a store
 // costs no 64-bit address arithmetic (a v_lshl_add_u64 per store with flat addresses).
-// MPPI_TRAJ_AUX is the store's cache-policy field (experiment knob, 0 = plain).
+// MPPI_TRAJ_AUX is the stores' cache-policy field: sc1 (device scope: written through
+// the XCD's L2) | nt (streaming).  With plain stores (0) the L2s hold up to 8 x 4 MB of
+// dirty trajectory lines when the waves finish, and the kernel-end release writes them
+// back serially: same-box A/B (profiles/r02/ab_store_policy.txt) whole-body K=8192 H=64
+// rollout 16.4 -> 12.8 us, arm C3 7.1 -> 6.0 us, V=8 fleet 93.7 -> 81.2 us.
 #ifndef MPPI_TRAJ_AUX
-#define MPPI_TRAJ_AUX 0
+#define MPPI_TRAJ_AUX 18
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t traj_rsrc(float* planes_v, uint32_t plane_b, int C) {
     return __builtin_amdgcn_make_buffer_rsrc(planes_v, 0, (int)(plane_b * (uint32_t)C), 0x00020000);
@@ -420,6 +424,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t traj_rsrc(float* planes_v, uin
 __device__ __forceinline__ void traj_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, float x) {
     if (MPPI_KO & 16) return;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)voff, (int)soff, MPPI_TRAJ_AUX);
+}
+// The same policy for the record bodies the finalize reads (full 256 B t-runs): a raw
+// buffer over a wave-uniform base, byte offsets < 4 GiB.  NOT for S: its one-lane 4 B
+// stores become partial-line writes through to memory (whole-body K=8192 rollout
+// 13.7 -> 19.0 us, profiles/r02/ab_store_policy.txt); in L2 they merge into full lines.
+__device__ __forceinline__ void wt_store(float* base_uniform, uint32_t byte_off, float x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base_uniform, 0, (int)0xFFFFFFFFu, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)byte_off, 0, MPPI_TRAJ_AUX);
 }
 
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
@@ -1114,7 +1126,8 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
     // in fp32 is exact, the quotient's error (< 1e-5 for i < A*H <= 2560) being far below
     // the 1/(2H) margin; 32-bit record indices (V*A*nb*H < 2^31, checked at create).
     const float rH = 1.0f / (float)H;
-    const uint32_t rbase = ((uint32_t)v * NA * (uint32_t)p.nb + blockIdx.x) * (uint32_t)H;
+    float* const rdata_v = p.rdata + (size_t)v * NA * p.nb * H;   // this vehicle's bodies (< 1 GiB)
+    const uint32_t rbase = blockIdx.x * (uint32_t)H;
     const uint32_t rstride = (uint32_t)p.nb * (uint32_t)H;
     for (int i = tid; i < ((MPPI_KO & 64) ? 0 : HA); i += nthr) {
         const int a = (int)(((float)i + 0.5f) * rH), t = i - a * H;
@@ -1127,7 +1140,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
             for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
             s += fw[w] * sw;
         }
-        p.rdata[rbase + (uint32_t)a * rstride + (uint32_t)t] = s;
+        wt_store(rdata_v, (rbase + (uint32_t)a * rstride + (uint32_t)t) * 4u, s);
     }
     STAMP(7);
     STAMPRT(14);
