@@ -9,7 +9,7 @@
 using namespace mppi;
 
 // =============================================================================
-// k_finalize: grid (A*ts, V); block (a, slice) owns t in one slice of action
+// k_finalize: grid (Ga*ts, V), Ga = A rounded up to 8; block (a, slice) owns t in one slice of action
 // dim a of vehicle v (plus the SavGol halo it reads).
 //   1. rho = min_r rho_r                     (record headers)
 //   2. f_r = exp(-(rho_r - rho)/lambda); eta = sum f_r eta_r   (fp64 sums)
@@ -25,6 +25,14 @@ using namespace mppi;
 // K=8192 (512 records) best at 512.
 constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 waves)
 constexpr int kMaxRec = 4096;
+// timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
+// outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor)
+#ifndef MPPI_FIN_KO
+#define MPPI_FIN_KO 0
+#endif
+#ifndef MPPI_FIN_KWARM
+#define MPPI_FIN_KWARM 1
+#endif
 
 // DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
 // result lands in lane 63 and is broadcast with readlane (no LDS round trips).
@@ -65,7 +73,7 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
     do {                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                           \
         if (pk.stamps && threadIdx.x == 0)                                           \
-            pk.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps + (i)] = \
+            pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + (i)] =               \
                 __builtin_amdgcn_s_memtime();                                        \
         __builtin_amdgcn_sched_barrier(0);                                           \
     } while (0)
@@ -103,7 +111,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
     const int tsz = (int)(geo & 0xFFu), hf = (int)((geo >> 8) & 0xFFu), ts = (int)((geo >> 16) & 0xFFu);
     const int A = (int)(geo >> 24);
-    const int a = blockIdx.x / ts, sl = blockIdx.x - a * ts, v = blockIdx.y;
+    // XCD-aware block map: the dispatcher deals blocks round robin over the 8 XCDs, so
+    // block b = a + Ga*sl (Ga = A rounded up to 8) puts every slice of dim a on XCD a mod 8:
+    // the slices read the same record lines (one 128 B line holds 32 t of a row), which one
+    // L2 then fetches once instead of once per slice.  Blocks with a >= A exit at once.
+    const int Ga = (A + 7) & ~7;
+    const int sl = blockIdx.x / Ga, a = blockIdx.x - sl * Ga, v = blockIdx.y;
+    if (a >= A) return;
+    if (MPPI_FIN_KO & 16) { if (tid == 0) u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
     FSTAMP(0);
     const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
     const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
@@ -128,6 +143,15 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         x0f = vcp->pos0f[a]; v0f = vcp->vel0f[a]; x0d = vcp->pos0[a]; v0d = vcp->vel0[a];
     }
 
+    // touch every kernel-argument line the tail reads (one s_load per 64 B; the FinParams
+    // fields past the preloaded ones): the first load of a line comes from memory (~1.5k
+    // cycles), and the tail's scalar loads were waited for one after another
+    uint32_t kwarm = 0u;
+    if (MPPI_FIN_KWARM) {
+        const uint32_t* kp = (const uint32_t*)&pk;
+#pragma unroll
+        for (int o = 0; o < (int)(sizeof(FinParams) / 4); o += 16) kwarm ^= kp[o];
+    }
     float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
     double eta = 0.0, eta2 = 0.0;   // counted by the q == 0 column only
     for (int base = 0; base < n; base += TR * kNPT) {
@@ -144,6 +168,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
             xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
         }
+        // the kernel-argument lines arrive while the record loads are in flight
+        if (base == 0) asm volatile("" :: "s"(kwarm));
 #pragma unroll
         for (int i = 0; i < kNPT; ++i)
             if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
@@ -183,6 +209,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         if (lane == 0) { wrho[wv] = rw; wnan[wv] = nf; weta[wv] = e1; weta2[wv] = e2; }
     }
     FSTAMP(1);
+    if (MPPI_FIN_KO & 8) { if (lane < CW) u_prev[lane] += acc + (float)eta; return; }   // timing knockout
     lds_barrier();
     if (wv != 0) return;
     FSTAMP(2);
@@ -243,7 +270,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * A + a] = sm;
         up[t * A + a] = un;
     }
-    if (sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
+    if (!(MPPI_FIN_KO & 2) && sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
 #pragma clang fp contract(off)
         const float u0 = un;
         const float uold0 = u_old;
@@ -311,7 +338,7 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     int nt = 512;
     for (int c : {128, 256})
         if (c * 16 / cw >= p->nrec) { nt = c; break; }
-    const dim3 grid(p->A * p->ts, p->V), block(nt);
+    const dim3 grid(((p->A + 7) & ~7) * p->ts, p->V), block(nt);   // XCD-aware map (k_finalize)
     hipStream_t s = (hipStream_t)stream;
 #define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
     hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo, \
