@@ -30,9 +30,6 @@ constexpr int kMaxRec = 4096;
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
-#ifndef MPPI_FIN_KWARM
-#define MPPI_FIN_KWARM 1
-#endif
 
 // DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
 // result lands in lane 63 and is broadcast with readlane (no LDS round trips).
@@ -143,15 +140,30 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         x0f = vcp->pos0f[a]; v0f = vcp->vel0f[a]; x0d = vcp->pos0[a]; v0d = vcp->vel0[a];
     }
 
-    // touch every kernel-argument line the tail reads (one s_load per 64 B; the FinParams
-    // fields past the preloaded ones): the first load of a line comes from memory (~1.5k
-    // cycles), and the tail's scalar loads were waited for one after another
-    uint32_t kwarm = 0u;
-    if (MPPI_FIN_KWARM) {
-        const uint32_t* kp = (const uint32_t*)&pk;
+    // The tail's kernel arguments (FinParams fields past the preloaded ones), read into
+    // SGPRs while the record loads fly: left to the compiler, each was an s_load waited
+    // for on the spot in wave 0's tail (15 serial scalar round trips).  The empty asm
+    // makes every value opaque, so it is neither re-loaded later nor sunk to its use.
+    float coef = 0.0f, dt = 0.0f, dt2 = 0.0f;
+    int32_t mode = 0, model = 0, qoff = 0, nq = 0, sf64 = 0, odim = 0;
+    uint32_t seq = 0;
+    float *wraw = nullptr, *wsmooth = nullptr, *u0p = nullptr, *stats = nullptr;
+    double* outp = nullptr;
+    uint32_t* flags = nullptr;
+    float sg[WIN > 0 ? WIN : 1];
+    auto pin_tail = [&]() {
+#define MPPI_PIN(x, f) do { x = f; asm volatile("" : "+s"(x)); } while (0)
+        MPPI_PIN(coef, p.coef); MPPI_PIN(dt, p.dt); MPPI_PIN(dt2, p.dt2);
+        MPPI_PIN(mode, p.mode); MPPI_PIN(model, p.model); MPPI_PIN(qoff, p.qoff); MPPI_PIN(nq, p.nq);
+        MPPI_PIN(sf64, p.state_f64); MPPI_PIN(odim, p.out_dim); MPPI_PIN(seq, p.seq);
+        MPPI_PIN(wraw, p.wraw); MPPI_PIN(wsmooth, p.wsmooth); MPPI_PIN(u0p, p.u0); MPPI_PIN(stats, p.stats);
+        MPPI_PIN(outp, p.out); MPPI_PIN(flags, p.flags);
+        if constexpr (WIN > 0) {
 #pragma unroll
-        for (int o = 0; o < (int)(sizeof(FinParams) / 4); o += 16) kwarm ^= kp[o];
-    }
+            for (int j = 0; j < WIN; ++j) MPPI_PIN(sg[j], p.sg[j]);
+        }
+#undef MPPI_PIN
+    };
     float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
     double eta = 0.0, eta2 = 0.0;   // counted by the q == 0 column only
     for (int base = 0; base < n; base += TR * kNPT) {
@@ -168,8 +180,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
             xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
         }
-        // the kernel-argument lines arrive while the record loads are in flight
-        if (base == 0) asm volatile("" :: "s"(kwarm));
+        if (base == 0) pin_tail();
 #pragma unroll
         for (int i = 0; i < kNPT; ++i)
             if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
@@ -180,7 +191,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         if (m < INFINITY) {
             const float rn = fminf(rho_t, m);
             if (rho_t < INFINITY) {   // rescale the running sums to the new reference
-                const float sc = __expf(p.coef * (rho_t - rn));
+                const float sc = __expf(coef * (rho_t - rn));
                 acc *= sc;
                 eta *= (double)sc;
                 eta2 *= (double)sc * (double)sc;
@@ -188,7 +199,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             rho_t = rn;
 #pragma unroll
             for (int i = 0; i < kNPT; ++i) {
-                const float f = (hd[i].x < INFINITY) ? __expf(p.coef * (hd[i].x - rn)) : 0.0f;
+                const float f = (hd[i].x < INFINITY) ? __expf(coef * (hd[i].x - rn)) : 0.0f;
                 acc = fmaf(f, xv[i], acc);
                 if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
             }
@@ -197,7 +208,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     }
     {   // fold the wave: rescale every lane to the wave's rho, sum the rows
         const float rw = wave_min(rho_t);
-        const float sc = (rho_t < INFINITY) ? __expf(p.coef * (rho_t - rw)) : 0.0f;
+        const float sc = (rho_t < INFINITY) ? __expf(coef * (rho_t - rw)) : 0.0f;
         acc *= sc;
         eta *= (double)sc;
         eta2 *= (double)sc * (double)sc;
@@ -221,7 +232,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     eta = 0.0; eta2 = 0.0;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) {
-        const float f = (wrho[w] < INFINITY) ? __expf(p.coef * (wrho[w] - rho)) : 0.0f;
+        const float f = (wrho[w] < INFINITY) ? __expf(coef * (wrho[w] - rho)) : 0.0f;
         N = fmaf(f, (lane < CW) ? wcol[w][lane] : 0.0f, N);
         eta += (double)f * weta[w];
         eta2 += (double)f * f * weta2[w];
@@ -229,7 +240,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(3);
     const int t = w0 + lane;              // this lane's time index (lanes < W)
     const bool own = lane < W && t >= t_lo && t < t_hi;
-    if (p.mode == 1) {   // PACK raw sums into this shard's exchange slot
+    if (mode == 1) {   // PACK raw sums into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
         if (a == 0 && sl == 0 && lane == 0) {
             dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanf;
@@ -249,14 +260,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // shuffles (taps beyond the window are zero), u += w_eps
     const float etaf = (nanf > 0.0f) ? NAN : (float)eta;
     const float w = __fdividef(N, etaf);
-    if (p.wraw && own) p.wraw[((size_t)v * H + t) * A + a] = w;
+    if (wraw && own) wraw[((size_t)v * H + t) * A + a] = w;
     FSTAMP(4);
     float sm = 0.0f;
     auto tap = [&](int j) {
         int idx = t + j - hf;
         idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
         const int src = min(max(idx - w0, 0), 63);
-        sm = fmaf(p.sg[j], __shfl(w, src), sm);
+        sm = fmaf(WIN > 0 ? sg[j < WIN ? j : 0] : p.sg[j], __shfl(w, src), sm);
     };
     if constexpr (WIN > 0) {
 #pragma unroll
@@ -267,41 +278,41 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(5);
     const float un = u_old + sm;
     if (own) {
-        if (p.wsmooth) p.wsmooth[((size_t)v * H + t) * A + a] = sm;
+        if (wsmooth) wsmooth[((size_t)v * H + t) * A + a] = sm;
         up[t * A + a] = un;
     }
     if (!(MPPI_FIN_KO & 2) && sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
 #pragma clang fp contract(off)
         const float u0 = un;
         const float uold0 = u_old;
-        p.u0[(size_t)v * A + a] = u0;
-        double* out = p.out + (size_t)v * p.out_dim;
-        const bool drone_dim = (p.model == MPPI_MODEL_DRONE) || (p.model == MPPI_MODEL_WHOLEBODY && a < 3);
-        if (p.model == MPPI_MODEL_QUADROTOR) {
+        u0p[(size_t)v * A + a] = u0;
+        double* out = outp + (size_t)v * odim;
+        const bool drone_dim = (model == MPPI_MODEL_DRONE) || (model == MPPI_MODEL_WHOLEBODY && a < 3);
+        if (model == MPPI_MODEL_QUADROTOR) {
             // coupled dims (thrust rotated by R(rpy)): the host forms the outputs from u0
             // (mppi_capi.cpp quad_outputs)
         } else if (drone_dim) {   // drone_mppi.py:168-169
             const float x0 = x0f, v0 = v0f;
-            const float xo = (x0 + v0 * p.dt) + (0.5f * u0) * p.dt2;
-            const float vo = v0 + p.dt * u0;
+            const float xo = (x0 + v0 * dt) + (0.5f * u0) * dt2;
+            const float vo = v0 + dt * u0;
             out[a] = xo;
             out[3 + a] = vo;
         } else {           // mppi.py:157-158 (qdes uses the OLD u_prev[0])
-            const int j = a - p.qoff;
-            const int base = (p.model == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
-            const float t1 = uold0 * p.dt;
-            const float t2 = ((0.5f * u0) * p.dt) * p.dt;
-            const float t3 = u0 * p.dt;
-            if (p.state_f64 && p.model == MPPI_MODEL_ARM) {
+            const int j = a - qoff;
+            const int base = (model == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
+            const float t1 = uold0 * dt;
+            const float t2 = ((0.5f * u0) * dt) * dt;
+            const float t3 = u0 * dt;
+            if (sf64 && model == MPPI_MODEL_ARM) {
                 out[base + j] = (x0d + (double)t1) + (double)t2;
-                out[base + p.nq + j] = v0d + (double)t3;
+                out[base + nq + j] = v0d + (double)t3;
             } else {
                 out[base + j] = (double)((x0f + t1) + t2);
-                out[base + p.nq + j] = (double)(v0f + t3);
+                out[base + nq + j] = (double)(v0f + t3);
             }
         }
         if (a == 0) {
-            float* st = p.stats + (size_t)v * 4;
+            float* st = stats + (size_t)v * 4;
             st[0] = rho;
             st[1] = (float)eta;
             st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
@@ -310,9 +321,9 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs).
         // seq == 0: nobody waits on this step (mppi_run_steps before its last step) -- no
         // system-scope fence, whose L2 writeback costs ~1.5 us of kernel time
-        if (p.seq != 0u) {
+        if (seq != 0u) {
             __threadfence_system();
-            __hip_atomic_store(p.flags + (size_t)v * A + a, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(flags + (size_t)v * A + a, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     FSTAMP(6);
