@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 4
+#define MPPI_ABI_VERSION 5
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
@@ -139,6 +139,9 @@ typedef struct {
     float quad_inertia[3];      /* diagonal body inertia 1.57, 3.93, 2.59                       */
     float quad_kd;              /* linear drag coefficient kd (0)                               */
     float quad_gravity;         /* g = (0, 0, -quad_gravity), 9.81                              */
+    int32_t quad_literal_jinv;  /* 1: steps t >= 1 integrate rpy += dt inv(J(rpy)) omega exactly as
+                                 * the commented loop (drone_mppi.py:73-76); 0 (default): J at
+                                 * every step (J maps body rates to Euler rates, drone.py:114-124) */
 } mppi_config;
 
 typedef enum {

@@ -21,7 +21,7 @@ NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 4
+ABI_VERSION = 5
 COMM_ID_BYTES = 128
 
 
@@ -50,7 +50,7 @@ class Config(C.Structure):
                 ("q_center", C.c_float * MAX_JOINTS), ("q_lower", C.c_float * MAX_JOINTS),
                 ("q_upper", C.c_float * MAX_JOINTS),
                 ("quad_mass", C.c_float), ("quad_inertia", C.c_float * 3), ("quad_kd", C.c_float),
-                ("quad_gravity", C.c_float)]
+                ("quad_gravity", C.c_float), ("quad_literal_jinv", C.c_int32)]
 
 
 class Link(C.Structure):

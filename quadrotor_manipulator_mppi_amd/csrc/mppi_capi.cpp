@@ -707,10 +707,10 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     nb = std::min(nb, groups);
     int iters = (groups + nb - 1) / nb;
     nb = (groups + iters - 1) / iters;
-    if (c.model == MPPI_MODEL_QUADROTOR) {   // k_rollout_quad: one wave of 64 rollouts per block
-        e->threads = 64;
-        nb = (e->K + 63) / 64;
-        iters = 1;
+    if (c.model == MPPI_MODEL_QUADROTOR) {   // k_rollout_quad: 16 rollouts (4 lanes each) per dynamics
+        e->threads = 256;                     // wave; 1 dynamics wave per block up to 1024 blocks, else 4
+        iters = ((e->K + 15) / 16 * e->V <= 1024) ? 1 : 4;   // (carried in DevParams::iters)
+        nb = (e->K + 16 * iters - 1) / (16 * iters);
     }
     if (nb > 4096) { delete e; return fail(MPPI_ERR_INVALID_ARG, "too many rollout blocks (%d)", nb); }
     const int P = (kHdr + e->A * H + 3) & ~3;
@@ -867,7 +867,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.sinv = e->d_sinv; p.gamma_t = e->d_gamma; p.jtraj = e->d_jtraj;
     p.q_inv_m = (float)(1.0 / (double)c.quad_mass);   // 1/self.m as a Python float, used in fp32
     for (int d = 0; d < 3; ++d) p.q_iinv[d] = (float)(1.0 / (double)c.quad_inertia[d]);
-    p.q_kd = c.quad_kd; p.q_g = c.quad_gravity;
+    p.q_kd = c.quad_kd; p.q_g = c.quad_gravity; p.q_literal_jinv = c.quad_literal_jinv ? 1 : 0;
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS

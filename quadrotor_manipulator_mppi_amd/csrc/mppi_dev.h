@@ -112,6 +112,8 @@ struct DevParams {
     float q_iinv[3];              // fp32(1 / I_ii), diagonal inertia
     float q_kd;                   // linear drag
     float q_g;                    // gravity magnitude, g = (0, 0, -q_g)
+    int32_t q_literal_jinv;       // t >= 1 applies inv(J) to the body rates, as the commented loop
+                                  // (drone_mppi.py:73-76); 0 = J at every step
 };
 constexpr int kStamps = 16;
 

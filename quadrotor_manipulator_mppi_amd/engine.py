@@ -63,7 +63,7 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
     reference ships disabled (cost_manager.py:83-87).  ``cost_weights`` overrides
     ``w_covar, cost_alpha, cost_gamma, w_center, w_joint_track, w_action,
     joint_limit_penalty``.  ``quad`` overrides the QUADROTOR rigid body: ``quad_mass``,
-    ``quad_inertia`` (3,), ``quad_kd``, ``quad_gravity``."""
+    ``quad_inertia`` (3,), ``quad_kd``, ``quad_gravity``, ``quad_literal_jinv``."""
     L = capi.lib()
     cfg = capi.Config()
     L.mppi_config_default(C.byref(cfg), MODELS[model])
@@ -94,6 +94,8 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
                 cfg.quad_inertia[d] = float(val[d])
         elif k in QUAD_FIELDS:
             setattr(cfg, k, float(val))
+        elif k == "quad_literal_jinv":   # drone_mppi.py:73-76 taken literally (inv(J) for t >= 1)
+            cfg.quad_literal_jinv = 1 if val else 0
         else:
             raise ValueError(f"unknown quadrotor parameter {k!r}")
     if savgol_window is not None:

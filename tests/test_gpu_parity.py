@@ -534,3 +534,26 @@ def test_trajectory_above_4gib_rejected_at_create():
         _engine(model="wholebody", n_samples=1 << 20, n_horizon=256)
     e = _engine(model="wholebody", n_samples=1 << 20, n_horizon=256, store_trajectory=False)
     e.close()
+
+
+def test_trajectory_between_2_and_4_gib():
+    """One vehicle's trajectory planes above 2 GiB (arm K=2^20 H=32: 19 planes x 128 MiB
+    = 2.4 GiB): the buffer-resource byte offsets past 2^31 (negative as the builtin's int)
+    address the upper planes.  The first and last samples' stored joint positions equal the
+    integration of their stored noise and their EE the oracle FK."""
+    from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain
+    chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
+    K, H = 1 << 20, 32
+    q0 = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]
+    base = [0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0]
+    e = _engine(model="arm", n_samples=K, n_horizon=H, store_noise=True, seed=11, state_f64=False)
+    e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    e.step(np.array(base + q0 + [0.0] * 7, np.float64))
+    ks = np.r_[0:4, K - 4:K]
+    eps = e.get_noise()[0][ks]
+    tr = e.get_trajectory()[0][ks]
+    e.close()
+    q = O.integrate(torch.from_numpy(eps), torch.tensor(q0), torch.zeros(7), 0.01)
+    _close(tr[..., :7], q.numpy(), atol=2e-6, what="q (K=2^20)")
+    ee = O.ee_world(chain, q, torch.tensor(base))
+    _close(tr[..., 7:], ee.numpy().reshape(len(ks), H, 16), atol=2e-5, what="EE (K=2^20)")

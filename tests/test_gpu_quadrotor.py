@@ -3,8 +3,14 @@ C-ABI) against the torch restatement ``oracle.mppi_oracle.quad_step`` on the sam
 injected noise.  PARITY UNPINNED with respect to the reference: it ships this model
 only as commented code (drone_mppi.py:57-83), so the oracle is the checker.
 
-Tolerances (sequential fp32 dynamics; the device uses <= 2 ulp polynomial sin/cos and
-sin/cos division for tan where torch calls sinf/cosf/tanf):
+Both integrations of the Euler angles are checked: J at every step (the default) and
+the commented loop's literal inv(J) for t >= 1 (``quad_literal_jinv``; the oracle calls
+torch.linalg.inv, the device the closed-form inverse).  K = 100 leaves a partial last
+block of the 16-rollout blocks; K = 20000 takes the 64-rollout blocks (4 dynamics waves).
+
+Tolerances (sequential fp32 dynamics; the device takes the hardware sin/cos after an
+exact reduction and one hardware reciprocal for tan and 1/cos, where torch calls
+sinf/cosf/tanf):
 * trajectory xyz / rpy: 5e-5 absolute over H <= 64 steps;
 * S: 1e-4 relative;
 * the reduction given the GPU's own S: 1e-5 relative; end to end within the softmin's
@@ -35,8 +41,10 @@ def _close(got, want, rtol=0.0, atol=0.0, what=""):
     assert not bad.any(), f"{what}: {bad.sum()}/{bad.size} off, max err {err.max():.3e}"
 
 
-@pytest.mark.parametrize("K,H,seed", [(256, 32, 0), (100, 64, 1), (64, 20, 2)])
-def test_quadrotor_matches_oracle(K, H, seed):
+@pytest.mark.parametrize("K,H,seed,literal", [(256, 32, 0, False), (100, 64, 1, False), (64, 20, 2, False),
+                                              (256, 32, 3, True), (100, 64, 4, True),
+                                              (20000, 32, 5, False)])   # > 1024 blocks of 16: 64 per block
+def test_quadrotor_matches_oracle(K, H, seed, literal):
     torch.manual_seed(seed)
     rng = np.random.default_rng(seed)
     x = [0.2, -0.1, 2.5, 0.05, -0.08, 0.7]
@@ -45,11 +53,11 @@ def test_quadrotor_matches_oracle(K, H, seed):
     u = np.zeros((H, 4), np.float32)
     u[:, 0] = 14.7 * 9.81
     u += rng.normal(0, 0.5, (H, 4)).astype(np.float32)
-    e = _engine(n_samples=K, n_horizon=H, noise="injected", sigma=SIG)
+    e = _engine(n_samples=K, n_horizon=H, noise="injected", sigma=SIG, quad={"quad_literal_jinv": literal})
     e.set_target(np.asarray(target, np.float32))
     for s in range(2):
         noise = O.draw_noise(K, H, torch.from_numpy(SIG))
-        ref = O.quad_step(x, v, torch.from_numpy(u), noise, target)
+        ref = O.quad_step(x, v, torch.from_numpy(u), noise, target, literal_jinv=literal)
         e.set_u_prev(u)
         out, u0, st = e.step(np.asarray(x + v, np.float64), noise.numpy()[None])
         _close(e.get_trajectory()[0], ref["traj"].numpy(), atol=5e-5, what="traj")

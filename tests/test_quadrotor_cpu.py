@@ -59,6 +59,29 @@ def test_jacobian_and_rotation_match_drone_py():
     assert np.allclose(R, Rz @ Ry @ Rx, atol=1e-12)
 
 
+def test_literal_jinv_closed_form():
+    """The device's literal mode (quad_literal_jinv) applies the closed-form inverse
+    [[1, 0, -s_th], [0, c_ph, s_ph c_th], [0, -s_ph, c_ph c_th]] where the commented loop
+    calls torch.linalg.inv(J) (drone_mppi.py:74); the oracle's literal rollout differs
+    from the J rollout once the body rates are nonzero."""
+    g = torch.Generator().manual_seed(5)
+    e = (torch.rand((512, 3), generator=g, dtype=torch.float64) - 0.5) * torch.tensor([3.0, 2.6, 6.0], dtype=torch.float64)
+    Ji = torch.linalg.inv(O.quad_jacobian(e))
+    ph, th = e[:, 0], e[:, 1]
+    z, o = torch.zeros_like(ph), torch.ones_like(ph)
+    Jc = torch.stack([torch.stack([o, z, -torch.sin(th)], -1),
+                      torch.stack([z, torch.cos(ph), torch.sin(ph) * torch.cos(th)], -1),
+                      torch.stack([z, -torch.sin(ph), torch.cos(ph) * torch.cos(th)], -1)], -2)
+    assert torch.allclose(Ji, Jc, atol=1e-9)
+    u = torch.zeros((1, 16, 4))
+    u[..., 0] = 14.7 * 9.81
+    u[..., 1:] = 0.5
+    a = O.quad_rollout(u, [0, 0, 1.0, 0.2, -0.3, 0.1], [0.0] * 6)
+    b = O.quad_rollout(u, [0, 0, 1.0, 0.2, -0.3, 0.1], [0.0] * 6, literal_jinv=True)
+    assert torch.equal(a[:, :1], b[:, :1])            # step 0 applies J in both (:69)
+    assert (a[:, 1:, 3:] - b[:, 1:, 3:]).abs().max() > 1e-6
+
+
 def test_tilted_thrust_accelerates_sideways():
     """Roll phi tilts body z toward -y: a_y = -g tan(phi) at the thrust that holds altitude."""
     phi = 0.2
