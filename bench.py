@@ -291,6 +291,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
         assert np.isfinite(out).all(), "non-finite control output"
     res = {"dt": dt, "tim": tim, "lat": lat, "K": eng.K, "H": eng.H, "A": eng.A, "V": V, "strong": strong,
            "bytes": eng.rollout_bytes(), "ess": float(st[0].ess), "cfg": eng.cfg, "native": se.native,
+           "native_error": se.native_error,
            "nranks": world}
     eng.close()
     return res
@@ -400,6 +401,7 @@ def main():
                     "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
                     if r["native"] else "torch.distributed all_reduce(SUM) of the slots"),
                 "allreduce_us": tim.get("allreduce_us"),
+                "native_comm_error": r["native_error"],
                 "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks"),
                 "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
         print(json.dumps(line), flush=True)

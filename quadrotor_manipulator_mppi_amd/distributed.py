@@ -21,6 +21,10 @@ Two ways to run the collective:
 * ``native=False``: the engine packs into a torch buffer and ``torch.distributed``
   does the all-reduce (any backend; the gloo tests on CPU and rehearsals use it).
 
+If the native communicator cannot be set up on some rank (no loadable RCCL, a bad
+unique id), every rank learns it (one MIN all-reduce of an ok flag) and all of them fall
+back to the torch.distributed collective on a fresh engine; ``native_error`` says why.
+
 The reference has no distributed code (single process, ``CUDA_VISIBLE_DEVICES='0'``
 at ``mppi.py:31``); there is no reference collective to mirror.
 """
@@ -50,13 +54,27 @@ def share_comm_id(rank: int, world: int, group=None, make_id: Optional[Callable[
     malformed id, so no rank enters the collective init with a bad one."""
     from . import _capi
     make_id = make_id or Engine.comm_unique_id
-    uid = [make_id() if rank == 0 else None]
+    uid = [None]
+    if rank == 0:
+        try:
+            uid[0] = make_id()
+        except Exception as exc:   # still broadcast: the other ranks must not wait forever
+            uid[0] = f"rank 0 could not make the RCCL unique id: {exc}"
     if world > 1:
         dist.broadcast_object_list(uid, src=0, group=group)
     if not isinstance(uid[0], (bytes, bytearray)) or len(uid[0]) != _capi.COMM_ID_BYTES:
-        raise RuntimeError(f"rank {rank}: bad RCCL unique id from rank 0 "
-                           f"({type(uid[0]).__name__}, {len(uid[0]) if uid[0] is not None else 0} bytes)")
+        why = uid[0] if isinstance(uid[0], str) else (
+            f"{type(uid[0]).__name__}, {len(uid[0]) if uid[0] is not None else 0} bytes")
+        raise RuntimeError(f"rank {rank}: bad RCCL unique id from rank 0 ({why})")
     return bytes(uid[0])
+
+
+def _all_ranks_ok(ok: bool, group, device: int) -> bool:
+    """True only if every rank passes ok (one MIN all-reduce over the process group)."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                     device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
 
 def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
@@ -93,9 +111,25 @@ class ShardedEngine:
         self.engine.set_stream(self.stream.cuda_stream)
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
+        self.native_error: Optional[str] = None
         if self.native:   # engine-owned RCCL communicator: the whole step is enqueued from C
-            self.engine.comm_init(share_comm_id(self.rank, self.world, group))
-        elif self.world > 1:
+            err = None
+            try:
+                self.engine.comm_init(share_comm_id(self.rank, self.world, group))
+            except Exception as exc:   # e.g. no loadable RCCL (every rank sees it: checked below)
+                err = str(exc)
+            if self.world > 1 and not _all_ranks_ok(err is None, group, self.local):
+                # a failure on any rank: every rank takes the torch.distributed collective
+                # instead (same slots, same finalize) on a fresh engine, so no rank is left
+                # waiting in a collective alone
+                self.native_error = err or "another rank failed mppi_comm_init"
+                self.native = False
+                self.engine.close()
+                self.engine = Engine(cfg)
+                self.engine.set_stream(self.stream.cuda_stream)
+            elif err is not None:
+                raise RuntimeError(err)
+        if not self.native and self.world > 1:
             slot = self.engine.exchange_slot_floats()
             with torch.cuda.stream(self.stream):
                 self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")

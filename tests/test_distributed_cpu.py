@@ -136,6 +136,8 @@ def _uid_rank(rank, world, port, q, bad):
 
         def make_id():
             made.append(rank)
+            if bad == "raise":
+                raise RuntimeError("librccl.so.1 not found")
             return b"x" * 7 if bad else bytes(range(128))
         try:
             q.put((rank, share_comm_id(rank, world, make_id=make_id), made))
@@ -145,11 +147,12 @@ def _uid_rank(rank, world, port, q, bad):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bad", [False, True])
+@pytest.mark.parametrize("bad", [False, True, "raise"])
 def test_comm_id_broadcast_world2(bad):
     """The engine-owned RCCL path's id hand-off (distributed.share_comm_id): only rank 0
     makes the ncclUniqueId, every rank receives the same 128 bytes over torch.distributed;
-    a malformed id is refused on every rank before ncclCommInitRank."""
+    a malformed id -- or rank 0 failing to make one -- is refused on every rank before
+    ncclCommInitRank (no rank is left waiting in the broadcast)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -164,6 +167,8 @@ def test_comm_id_broadcast_world2(bad):
     assert res[0][2] == [0] and res[1][2] == [], "only rank 0 makes the id"
     if bad:
         assert all("bad RCCL unique id" in r[1] for r in res)
+        if bad == "raise":
+            assert all("librccl.so.1 not found" in r[1] for r in res)
     else:
         assert res[0][1] == res[1][1] == bytes(range(128))
 
