@@ -19,6 +19,11 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libmppi_hip.so")
 LIB_STAMPS = os.path.join(LIB_DIR, "libmppi_hip_stamps.so")   # diagnostic phase-stamp build
+LIB_ASAN = os.path.join(LIB_DIR, "libmppi_hip_asan.so")       # host AddressSanitizer build (CPU tests only)
+# AddressSanitizer on the HOST side of every translation unit only (-Xarch_host): the device
+# code is unchanged, and the library runs the CPU tests with the runtime preloaded
+# (scripts/asan_cpu_tests.sh).  GPU sanitizers are not available on the GPU pool.
+_ASAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
 # (source, extra flags).  The rollout is built without the SLP vectorizer: its
 # v_pk_* pairings cost more register moves than they save and raise the kernel
 # from 110 to 184 VGPRs (2 instead of 4 waves per SIMD) -- DESIGN.md §kernels.
@@ -50,16 +55,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, debug: bool = False, verbose: bool = False, stamps: bool = False) -> str:
-    out = os.environ.get("MPPI_BUILD_OUT") or (LIB_STAMPS if stamps else LIB)
-    if not force and not stamps and not _stale():
+def build(force: bool = False, debug: bool = False, verbose: bool = False, stamps: bool = False,
+          asan: bool = False) -> str:
+    out = os.environ.get("MPPI_BUILD_OUT") or (LIB_STAMPS if stamps else LIB_ASAN if asan else LIB)
+    if not force and not stamps and not asan and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = out + ".tmp"
     base = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O1" if debug else "-O3",
             "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-Wno-unused-variable"] + \
-        (["-DMPPI_STAMPS"] if stamps else []) + EXTRA
-    objdir = os.path.join(LIB_DIR, "obj" + ("_stamps" if stamps else ""))
+        (["-DMPPI_STAMPS"] if stamps else []) + (_ASAN if asan else []) + EXTRA
+    objdir = os.path.join(LIB_DIR, "obj" + ("_stamps" if stamps else "_asan" if asan else ""))
     os.makedirs(objdir, exist_ok=True)
     objs, procs = [], []
     for src, flags in SOURCES:   # compile the translation units in parallel
@@ -75,7 +81,8 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False, stamp
             raise RuntimeError(f"hipcc failed on {src} ({pr.returncode}):\n{so}\n{se}")
         if verbose and se.strip():
             print(se)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + \
+        (["-Xarch_host", "-fsanitize=address", "-shared-libsan"] if asan else [])
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
@@ -112,6 +119,7 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="diagnostic build with per-phase s_memtime stamps")
+    ap.add_argument("--asan", action="store_true", help="host AddressSanitizer build (lib/libmppi_hip_asan.so)")
     a = ap.parse_args()
-    print(build(force=a.force, debug=a.debug, verbose=True, stamps=a.stamps))
+    print(build(force=a.force, debug=a.debug, verbose=True, stamps=a.stamps, asan=a.asan))
     sys.exit(0)
