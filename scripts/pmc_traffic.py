@@ -46,7 +46,13 @@ def main():
         except (OSError, ValueError):
             allw = {}
         roll = next((rec[k] for k in sorted(rec) if k.startswith("k_rollout")), {})
+        try:   # the library build the counters were collected on (build.py writes BUILD_INFO.json)
+            head = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "quadrotor_manipulator_mppi_amd", "lib", "BUILD_INFO.json")))["git_head"]
+        except (OSError, ValueError, KeyError):
+            head = "?"
         allw[workload] = {"hbm_bytes_per_launch": roll.get("hbm_bytes_per_launch"), "kernels": rec,
+                          "build_head": head, "collected": root,
                           "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes, avg per dispatch"}
         json.dump(allw, open(out, "w"), indent=1)
 
