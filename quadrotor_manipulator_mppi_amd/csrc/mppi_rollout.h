@@ -125,36 +125,44 @@ __host__ __device__ __forceinline__ uint32_t philox2_key(uint32_t seed_lo, uint3
 //     (kg, veh<<8 | t), key philox2_key(seed, step), its words giving pairs 8J.., 8J+2..
 //     (J = NA/8); r >= 5 -> Philox4x32-10 call J as above.
 // (the whole-body's 10 dims: one 4x32 call + one 2x32 call, 30 multiplies instead of 40)
+// The draw in two halves (the rollout overlaps them with LDS latency, k_rollout): the
+// Philox words of one (k, t) -- word 4j + i of call j, then the Philox2x32 words -- and the
+// normals Box-Muller makes of them.
 template <int NA>
-__device__ __forceinline__ void draw_normals(float (&z)[NA], uint32_t kg, uint32_t t, uint32_t veh,
-                                             uint32_t step, uint32_t s0, uint32_t s1) {
+constexpr int draw_words() {
+    return 4 * (NA / 8 + ((NA % 8) >= 5 ? 1 : 0)) + (((NA % 8) >= 1 && (NA % 8) <= 4) ? 2 : 0);
+}
+template <int NA>
+__device__ __forceinline__ void draw_philox(uint32_t (&w)[draw_words<NA>()], uint32_t kg, uint32_t t, uint32_t veh,
+                                            uint32_t step, uint32_t s0, uint32_t s1) {
     constexpr int J = NA / 8, REM = NA % 8;
     constexpr int N4 = J + (REM >= 5 ? 1 : 0);   // Philox4x32 calls
 #pragma unroll
     for (int j = 0; j < N4; ++j) {
-        uint32_t w[4] = {kg, t, (veh << 8) | (uint32_t)j, step};
-        if (!(MPPI_KO & 2)) philox10(w[0], w[1], w[2], w[3], s0, s1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (8 * j + 2 * i >= NA) break;
-            float a, b;
-            box_muller32(w[i], a, b);
-            z[8 * j + 2 * i] = a;
-            if (8 * j + 2 * i + 1 < NA) z[8 * j + 2 * i + 1] = b;
-        }
+        w[4 * j] = kg; w[4 * j + 1] = t; w[4 * j + 2] = (veh << 8) | (uint32_t)j; w[4 * j + 3] = step;
+        if (!(MPPI_KO & 2)) philox10(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3], s0, s1);
     }
     if constexpr (REM >= 1 && REM <= 4) {
-        uint32_t w[2] = {kg, (veh << 8) | t};
-        if (!(MPPI_KO & 2)) philox2x10(w[0], w[1], philox2_key(s0, s1, step));
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            if (8 * J + 2 * i >= NA) break;
-            float a, b;
-            box_muller32(w[i], a, b);
-            z[8 * J + 2 * i] = a;
-            if (8 * J + 2 * i + 1 < NA) z[8 * J + 2 * i + 1] = b;
-        }
+        w[4 * N4] = kg; w[4 * N4 + 1] = (veh << 8) | t;
+        if (!(MPPI_KO & 2)) philox2x10(w[4 * N4], w[4 * N4 + 1], philox2_key(s0, s1, step));
     }
+}
+template <int NA>
+__device__ __forceinline__ void draw_box_muller(const uint32_t (&w)[draw_words<NA>()], float (&z)[NA]) {
+#pragma unroll
+    for (int i = 0; 2 * i < NA; ++i) {   // word i gives normals 2i, 2i + 1 (both layouts above)
+        float a, b;
+        box_muller32(w[i], a, b);
+        z[2 * i] = a;
+        if (2 * i + 1 < NA) z[2 * i + 1] = b;
+    }
+}
+template <int NA>
+__device__ __forceinline__ void draw_normals(float (&z)[NA], uint32_t kg, uint32_t t, uint32_t veh,
+                                             uint32_t step, uint32_t s0, uint32_t s1) {
+    uint32_t w[draw_words<NA>()];
+    draw_philox<NA>(w, kg, t, veh, step, s0, s1);
+    draw_box_muller<NA>(w, z);
 }
 
 // Philox words one (k, t) draw consumes (the raw layout of k_philox / oracle.philox_normals)
@@ -521,10 +529,14 @@ __device__ __forceinline__ float row_shr_f32(float x) {   // out-of-row sources 
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
 }
 
-// inc[a] (lane = segment*L + t) = q(t) - q0 for the controls act[a] of this lane
-template <int L, int NA>
+// inc[a] (lane = segment*L + t) = q(t) - q0 for the controls act[a] of this lane.
+// fill1 / fill2 run while the transposed reads and the increments' reads are in flight
+// (independent VALU work of the caller: the next rollout group's noise draw).
+struct NoFill { __device__ void operator()() const {} };
+template <int L, int NA, typename F1 = NoFill, typename F2 = NoFill>
 __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw, const int lane, const float dt,
-                                              const float dt2h, const float* vel0f, float (&inc)[NA]) {
+                                              const float dt2h, const float* vel0f, float (&inc)[NA],
+                                              F1&& fill1 = NoFill(), F2&& fill2 = NoFill()) {
     using G = IntegGeom<L, NA>;
     constexpr int P = G::P, CPS = G::CPS, CL = G::CL, S = G::S;
 #pragma unroll
@@ -534,10 +546,13 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     const bool on = sr < S;
     const int seg = sr / NA, a = sr - seg * NA;
     const int rb = on ? (seg * L + ch * CL) * P + a : 0;
-    float lv = 0.0f, lp = 0.0f, loc[CL];
+    float lv = 0.0f, lp = 0.0f, loc[CL], xin[CL];
+#pragma unroll
+    for (int i = 0; i < CL; ++i) xin[i] = xw[rb + i * P];
+    fill1();
 #pragma unroll
     for (int i = 0; i < CL; ++i) {
-        const float x = xw[rb + i * P];
+        const float x = xin[i];
         lp += fmaf(lv, dt, x * dt2h);
         lv = fmaf(x, dt, lv);
         loc[i] = lp;
@@ -563,6 +578,7 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     wave_lds_handoff();
 #pragma unroll
     for (int a2 = 0; a2 < NA; ++a2) inc[a2] = xw[lane * P + a2];
+    fill2();
 }
 
 // The leading scalar arguments are preloaded into SGPRs at wave launch on gfx950
@@ -586,6 +602,13 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
     constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
     constexpr int kJW = (int)(sizeof(JointDev) * kMaxJ / 4);   // joint table, dwords
+    // looping kernel, one chunk: group it + 1's normals are drawn inside group it's
+    // integrator, whose LDS round trips otherwise leave the SIMD idle (the 4 waves of a
+    // SIMD reach them together); MPPI_PIPE=0 draws them at the start of each group
+#ifndef MPPI_PIPE
+#define MPPI_PIPE 1
+#endif
+    constexpr bool kPipe = MPPI_PIPE && NCH == 1 && !ONEG && !(MPPI_KO & 1);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // Scalars and (V == 1) the vehicle constants are read from the kernel
     // arguments with scalar loads (SGPR operands, no LDS latency in the hot
@@ -713,7 +736,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
                 for (int a = 0; a < NA; ++a) eps[c][a] = src[a];
             } else {
                 float z[NA];
-                if (it == 0) {
+                if (it == 0 || kPipe) {   // drawn in the prologue / during the previous group
 #pragma unroll
                     for (int a = 0; a < NA; ++a) z[a] = z0[c][a];
                 } else {
@@ -797,7 +820,19 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
         double posd[NCH][F64 ? NA : 1];
         if constexpr (NCH == 1 && !(MPPI_KO & 1)) {
             float inc[NA];
-            integrate_lds<LSEG, NA>(act[0], xw, lane, p.dt, 0.5f * p.dt2, vc.vel0f, inc);
+            // the next group's normals fill the integrator's two LDS round trips (kPipe)
+            const bool pipe = kPipe && noise_mode != MPPI_NOISE_INJECTED && it + 1 < p.iters;
+            uint32_t wn[draw_words<NA>()];
+            auto fill1 = [&]() {
+                if (pipe) {
+                    const uint32_t kgn = k_off + (uint32_t)(((blockIdx.x + (it + 1) * p.nb) * nw + wid) * R + sub);
+                    draw_philox<NA>(wn, kgn, (uint32_t)t0, (uint32_t)v, step_ctr, seed_lo, seed_hi);
+                }
+            };
+            auto fill2 = [&]() {
+                if (pipe) draw_box_muller<NA>(wn, z0[0]);
+            };
+            integrate_lds<LSEG, NA>(act[0], xw, lane, p.dt, 0.5f * p.dt2, vc.vel0f, inc, fill1, fill2);
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 if (!F64) {
