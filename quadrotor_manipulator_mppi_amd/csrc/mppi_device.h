@@ -22,6 +22,15 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Hand-off between lanes of one wave through LDS: a wave's LDS instructions execute in
+// order, so no s_waitcnt is needed; the wavefront-scope fences order the accesses in the
+// memory model and keep the compiler from moving them (rocPRIM's wave_barrier idiom).
+__device__ __forceinline__ void wave_lds_handoff() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ----------------------------------------------------------------- DPP helpers
 // dpp_ctrl encodings (GFX9): row_shr:n = 0x110+n, wave_shr:1 = 0x138,
 // row_bcast:15 = 0x142, row_bcast:31 = 0x143.

@@ -31,39 +31,27 @@ constexpr int kMaxRec = 4096;
 #define MPPI_FIN_KO 0
 #endif
 
-// DPP wave reductions: the identity is fed to out-of-row / masked lanes, the
-// result lands in lane 63 and is broadcast with readlane (no LDS round trips).
-template <int CTRL, int RM>
-__device__ __forceinline__ float dpp_id(float x, float id) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(x), CTRL, RM, 0xF, false));
+// Folds over the row groups of a wave (lane = g * CW + q; ROWS = 64 / CW groups) with the
+// gfx950 lane swaps: v_permlane16_swap exchanges odd rows of one operand with even rows of
+// the other, v_permlane32_swap the halves.  With both operands = x, the two results hold
+// the partner rows' values, so op(r0, r1) is the pairwise fold in every lane (bit-identical
+// across the partners: op is commutative).  Two VALU ops per level instead of an LDS-pipe
+// ds_bpermute / ds_swizzle round trip; every lane of column q ends with the fold of q.
+template <int CW, typename Op>
+__device__ __forceinline__ float fold_rows(float x, Op op) {
+    if constexpr (CW <= 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    }
+    if constexpr (CW <= 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    }
+    return x;
 }
-__device__ __forceinline__ float wave_min(float x) {
-    x = fminf(x, dpp_id<0x111, 0xF>(x, INFINITY));
-    x = fminf(x, dpp_id<0x112, 0xF>(x, INFINITY));
-    x = fminf(x, dpp_id<0x114, 0xF>(x, INFINITY));
-    x = fminf(x, dpp_id<0x118, 0xF>(x, INFINITY));
-    x = fminf(x, dpp_id<0x142, 0xA>(x, INFINITY));
-    x = fminf(x, dpp_id<0x143, 0xC>(x, INFINITY));
-    return read_lane_f32(x, 63);
-}
-__device__ __forceinline__ float wave_max(float x) {
-    x = fmaxf(x, dpp_id<0x111, 0xF>(x, -INFINITY));
-    x = fmaxf(x, dpp_id<0x112, 0xF>(x, -INFINITY));
-    x = fmaxf(x, dpp_id<0x114, 0xF>(x, -INFINITY));
-    x = fmaxf(x, dpp_id<0x118, 0xF>(x, -INFINITY));
-    x = fmaxf(x, dpp_id<0x142, 0xA>(x, -INFINITY));
-    x = fmaxf(x, dpp_id<0x143, 0xC>(x, -INFINITY));
-    return read_lane_f32(x, 63);
-}
-__device__ __forceinline__ double wave_sum_f64(double x) {
-    x += shr_f64<0x111>(x);
-    x += shr_f64<0x112>(x);
-    x += shr_f64<0x114>(x);
-    x += shr_f64<0x118>(x);
-    x += dpp_f64<0x142, 0xA>(x);
-    x += dpp_f64<0x143, 0xC>(x);
-    return read_lane_f64(x, 63);
-}
+struct OpAdd { __device__ float operator()(float a, float b) const { return a + b; } };
+struct OpMin { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
+struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
 
 #ifdef MPPI_STAMPS
 #define FSTAMP(i)                                                                    \
@@ -101,8 +89,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     constexpr int TR = NWV * ROWS;         // rows per block
     constexpr int kNPT = 16;
     __shared__ float wcol[NWV][CW];
-    __shared__ float wrho[NWV], wnan[NWV];
-    __shared__ double weta[NWV], weta2[NWV];
+    __shared__ float wrho[NWV], wnan[NWV], weta[NWV], weta2[NWV];
+    __shared__ float wsg[96];   // wave 0: w over the window + reflected pads (SavGol taps by LDS reads)
     const FinParams& p = pk;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
@@ -164,8 +152,11 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         }
 #undef MPPI_PIN
     };
-    float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f;
-    double eta = 0.0, eta2 = 0.0;   // counted by the q == 0 column only
+    // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
+    // column of a row group, so each lane carries them and the wave fold runs over row groups
+    // only.  eta in fp32, like the reference's torch.sum of the fp32 exponentials
+    // (mppi.py:184-188): <= 16 terms per lane, then 2 + 3 (8 waves) folds.
+    float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f, eta = 0.0f, eta2 = 0.0f;
     for (int base = 0; base < n; base += TR * kNPT) {
         float4 hd[kNPT];
         float xv[kNPT];
@@ -193,29 +184,26 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             if (rho_t < INFINITY) {   // rescale the running sums to the new reference
                 const float sc = __expf(coef * (rho_t - rn));
                 acc *= sc;
-                eta *= (double)sc;
-                eta2 *= (double)sc * (double)sc;
+                eta *= sc;
+                eta2 *= sc * sc;
             }
             rho_t = rn;
 #pragma unroll
             for (int i = 0; i < kNPT; ++i) {
                 const float f = (hd[i].x < INFINITY) ? __expf(coef * (hd[i].x - rn)) : 0.0f;
                 acc = fmaf(f, xv[i], acc);
-                if (q == 0) { eta += (double)f * hd[i].y; eta2 += (double)f * f * hd[i].z; }
+                eta = fmaf(f, hd[i].y, eta);
+                eta2 = fmaf(f * f, hd[i].z, eta2);
             }
         }
         FSTAMP(8);
     }
-    {   // fold the wave: rescale every lane to the wave's rho, sum the rows
-        const float rw = wave_min(rho_t);
+    {   // fold the wave's row groups: rescale every lane to the wave's rho, sum the rows
+        const float rw = fold_rows<CW>(rho_t, OpMin());
         const float sc = (rho_t < INFINITY) ? __expf(coef * (rho_t - rw)) : 0.0f;
-        acc *= sc;
-        eta *= (double)sc;
-        eta2 *= (double)sc * (double)sc;
-        if (CW <= 16) acc += __shfl_xor(acc, 16);
-        if (CW <= 32) acc += __shfl_xor(acc, 32);
-        const double e1 = wave_sum_f64(eta), e2 = wave_sum_f64(eta2);
-        const float nf = wave_max(nanflag);
+        acc = fold_rows<CW>(acc * sc, OpAdd());
+        const float e1 = fold_rows<CW>(eta * sc, OpAdd()), e2 = fold_rows<CW>(eta2 * (sc * sc), OpAdd());
+        const float nf = fold_rows<CW>(nanflag, OpMax());
         if (lane < CW) wcol[wv][lane] = acc;
         if (lane == 0) { wrho[wv] = rw; wnan[wv] = nf; weta[wv] = e1; weta2[wv] = e2; }
     }
@@ -229,13 +217,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
 #pragma unroll
     for (int w = 1; w < NWV; ++w) { rho = fminf(rho, wrho[w]); nanf = fmaxf(nanf, wnan[w]); }
     float N = 0.0f;
-    eta = 0.0; eta2 = 0.0;
+    eta = 0.0f; eta2 = 0.0f;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) {
         const float f = (wrho[w] < INFINITY) ? __expf(coef * (wrho[w] - rho)) : 0.0f;
         N = fmaf(f, (lane < CW) ? wcol[w][lane] : 0.0f, N);
-        eta += (double)f * weta[w];
-        eta2 += (double)f * f * weta2[w];
+        eta = fmaf(f, weta[w], eta);
+        eta2 = fmaf(f * f, weta2[w], eta2);
     }
     FSTAMP(3);
     const int t = w0 + lane;              // this lane's time index (lanes < W)
@@ -243,7 +231,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     if (mode == 1) {   // PACK raw sums into this shard's exchange slot
         float* dst = p.dst + (size_t)v * p.P;
         if (a == 0 && sl == 0 && lane == 0) {
-            dst[0] = rho; dst[1] = (float)eta; dst[2] = (float)eta2; dst[3] = nanf;
+            dst[0] = rho; dst[1] = eta; dst[2] = eta2; dst[3] = nanf;
         }
         if (own) dst[kHdr + a * H + t] = N;
         for (int s = 0; s < p.nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
@@ -255,25 +243,32 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         return;
     }
 
-    // FINAL: w_eps = N/eta over the window, SavGol with the reference's symmetric
-    // pad (svg_filter.py:58: index -i-1 left of 0, 2H-1-i right of H-1) by lane
-    // shuffles (taps beyond the window are zero), u += w_eps
-    const float etaf = (nanf > 0.0f) ? NAN : (float)eta;
+    // FINAL: w_eps = N/eta over the window, SavGol, u += w_eps
+    const float etaf = (nanf > 0.0f) ? NAN : eta;
     const float w = __fdividef(N, etaf);
     if (wraw && own) wraw[((size_t)v * H + t) * A + a] = w;
     FSTAMP(4);
+    // SavGol with the reference's symmetric pad (svg_filter.py:58: index -i-1 left of 0,
+    // 2H-1-i right of H-1; one reflection suffices, create checks H > window/2): w goes to
+    // LDS at kPad + (t - w0), and the lanes within hf of an edge of the horizon also write
+    // their mirror position, so every owned lane reads its WIN taps at consecutive addresses
+    // (immediate offsets, one wait) -- no per-tap index arithmetic, no ds_bpermute.
+    constexpr int kPad = 8;   // >= hf (window <= 17)
     float sm = 0.0f;
-    auto tap = [&](int j) {
-        int idx = t + j - hf;
-        idx = idx < 0 ? -idx - 1 : (idx >= H ? 2 * H - 1 - idx : idx);
-        const int src = min(max(idx - w0, 0), 63);
-        sm = fmaf(WIN > 0 ? sg[j < WIN ? j : 0] : p.sg[j], __shfl(w, src), sm);
-    };
-    if constexpr (WIN > 0) {
+    if (lane < W) {
+        wsg[kPad + lane] = w;
+        if (w0 == 0 && t < hf) wsg[kPad - 1 - t] = w;                      // left pad
+        if (w1 == H && t >= H - hf) wsg[kPad + 2 * H - 1 - t - w0] = w;    // right pad
+    }
+    wave_lds_handoff();
+    {
+        const float* src = wsg + kPad + lane - hf;
+        if constexpr (WIN > 0) {
 #pragma unroll
-        for (int j = 0; j < WIN; ++j) tap(j);
-    } else {
-        for (int j = 0; j < p.window; ++j) tap(j);
+            for (int j = 0; j < WIN; ++j) sm = fmaf(sg[j], src[j], sm);
+        } else {
+            for (int j = 0; j < p.window; ++j) sm = fmaf(p.sg[j], src[j], sm);
+        }
     }
     FSTAMP(5);
     const float un = u_old + sm;
@@ -314,8 +309,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         if (a == 0) {
             float* st = stats + (size_t)v * 4;
             st[0] = rho;
-            st[1] = (float)eta;
-            st[2] = (eta2 > 0.0) ? (float)(eta * eta / eta2) : 0.0f;
+            st[1] = eta;
+            st[2] = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
             st[3] = nanf;
         }
         // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs).

@@ -515,15 +515,6 @@ constexpr int wave_slot_floats() {
                                                                      : 4 + NCH * 64 * NA;
 }
 
-// Hand-off between lanes of one wave through LDS: a wave's LDS instructions execute in
-// order, so no s_waitcnt is needed; the wavefront-scope fences order the accesses in the
-// memory model and keep the compiler from moving them (rocPRIM's wave_barrier idiom).
-__device__ __forceinline__ void wave_lds_handoff() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int CTRL>
 __device__ __forceinline__ float row_shr_f32(float x) {   // out-of-row sources read 0
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
