@@ -64,4 +64,42 @@ __device__ __forceinline__ float read_lane_f32(float x, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 
+// Folds over the row groups of a wave (lane = g * CW + q; ROWS = 64 / CW groups) with the
+// gfx950 lane swaps: v_permlane16_swap exchanges odd rows of one operand with even rows of
+// the other, v_permlane32_swap the halves.  With both operands = x, the two results hold
+// the partner rows' values, so op(r0, r1) is the pairwise fold in every lane (bit-identical
+// across the partners: op is commutative).  Two VALU ops per level instead of an LDS-pipe
+// ds_bpermute / ds_swizzle round trip; every lane of column q ends with the fold of q.
+template <int CW, typename Op>
+__device__ __forceinline__ float fold_rows(float x, Op op) {
+    if constexpr (CW <= 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    }
+    if constexpr (CW <= 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    }
+    return x;
+}
+struct OpAdd { __device__ float operator()(float a, float b) const { return a + b; } };
+struct OpMin { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
+struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+
+// The fold of a whole wave in every lane: quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
+// row_mirror, then the row-group swaps.  Every level pairs lanes symmetrically, so all 64
+// lanes end with the same bits (six VALU/DPP levels instead of six ds_bpermute round trips).
+template <int CTRL>
+__device__ __forceinline__ float dpp_all(float x) {   // CTRL with a valid source for every lane
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <typename Op>
+__device__ __forceinline__ float wave_fold_all(float x, Op op) {
+    x = op(x, dpp_all<0xB1>(x));    // quad_perm [1,0,3,2]
+    x = op(x, dpp_all<0x4E>(x));    // quad_perm [2,3,0,1]
+    x = op(x, dpp_all<0x141>(x));   // row_half_mirror
+    x = op(x, dpp_all<0x140>(x));   // row_mirror
+    return fold_rows<16>(x, op);
+}
+
 }  // namespace

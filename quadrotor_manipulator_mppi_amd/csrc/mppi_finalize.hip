@@ -31,28 +31,6 @@ constexpr int kMaxRec = 4096;
 #define MPPI_FIN_KO 0
 #endif
 
-// Folds over the row groups of a wave (lane = g * CW + q; ROWS = 64 / CW groups) with the
-// gfx950 lane swaps: v_permlane16_swap exchanges odd rows of one operand with even rows of
-// the other, v_permlane32_swap the halves.  With both operands = x, the two results hold
-// the partner rows' values, so op(r0, r1) is the pairwise fold in every lane (bit-identical
-// across the partners: op is commutative).  Two VALU ops per level instead of an LDS-pipe
-// ds_bpermute / ds_swizzle round trip; every lane of column q ends with the fold of q.
-template <int CW, typename Op>
-__device__ __forceinline__ float fold_rows(float x, Op op) {
-    if constexpr (CW <= 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    }
-    if constexpr (CW <= 32) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-        x = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
-    }
-    return x;
-}
-struct OpAdd { __device__ float operator()(float a, float b) const { return a + b; } };
-struct OpMin { __device__ float operator()(float a, float b) const { return fminf(a, b); } };
-struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
-
 #ifdef MPPI_STAMPS
 #define FSTAMP(i)                                                                    \
     do {                                                                             \

@@ -67,17 +67,6 @@ __device__ __forceinline__ float qsum(float x) {
     x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));   // [2,3,0,1]
     return x;
 }
-__device__ __forceinline__ float wave_min_f32(float x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o));
-    return x;
-}
-__device__ __forceinline__ float wave_sum_f32(float x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-
 }  // namespace
 
 // NWD dynamics waves per block (1 or 4): 16 rollouts per block while the grid stays at most
@@ -264,8 +253,8 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
     if (kval && j == 0) p.S[(size_t)v * K + k] = S;
     // ---- online softmin over the block's rollouts (mppi.py:184-188 / drone_mppi.py:111-130)
     const bool mine = kval && j == 0, bad = S != S;
-    float rho = wave_min_f32((mine && !bad) ? S : INFINITY);
-    float nanf = wave_sum_f32(mine && bad ? 1.0f : 0.0f) > 0.0f ? 1.0f : 0.0f;
+    float rho = wave_fold_all((mine && !bad) ? S : INFINITY, OpMin());
+    float nanf = wave_fold_all(mine && bad ? 1.0f : 0.0f, OpMax());
     if constexpr (NWD > 1) {
         if (lane == 0) { wred[wid][0] = rho; wred[wid][3] = nanf; }
         __syncthreads();
@@ -273,7 +262,7 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
         for (int w = 0; w < NWD; ++w) { rho = fminf(rho, wred[w][0]); nanf = fmaxf(nanf, wred[w][3]); }
     }
     const float e = (mine && !bad && rho < INFINITY) ? __expf(scoef * (S - rho)) : 0.0f;
-    float eta = wave_sum_f32(e), eta2 = wave_sum_f32(e * e);
+    float eta = wave_fold_all(e, OpAdd()), eta2 = wave_fold_all(e * e, OpAdd());
     if (j == 0) e_lds[r] = e;
     wave_lds_handoff();
     // ---- record N[a][t] = sum_k e_k eps_k[t][a], lane = t (each wave its own 16 rollouts)
