@@ -318,6 +318,9 @@ def main():
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=2.5, help="seconds of CPU sampling per baseline cell")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the event-timed kernel loops (profiler runs: the trace then holds only the "
+                         "control steps); no roofline in the line")
     ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
@@ -344,14 +347,15 @@ def main():
     from quadrotor_manipulator_mppi_amd import _capi
     _capi.lib()
 
-    r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps)
+    r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
+                     timing=not args.no_kernel_timing)
     K, H, V = r["K"], r["H"], r["V"]
     per_step = r["dt"] / args.steps
     value = world * V * K * H / per_step
     tim = r["tim"]
     lat = np.array(r["lat"]) * 1e3
     secondary = {}
-    if world == 1 and args.secondary:
+    if world == 1 and args.secondary and tim is not None:
         for wname in [s for s in args.secondary.split(",") if s and s != workload]:
             ns = max(50, args.steps // 5)
             s = run_workload(wname, ns, 20, 1, None, 50)
@@ -370,8 +374,9 @@ def main():
         log(f"cpu baseline: {cpu}")
     if rank == 0:
         traffic, traffic_src = load_traffic(workload)
-        rf = roofline_of(r)
-        rf.update({"traffic": traffic, "traffic_source": traffic_src})
+        rf = roofline_of(r) if tim is not None else None
+        if rf is not None:
+            rf.update({"traffic": traffic, "traffic_source": traffic_src})
         desc = WORKLOADS[workload]["desc"]
         line = {
             "metric": "MPPI rollouts/sec (K x H state-steps) + control-step p50 latency, K=4096 H=32",
@@ -388,7 +393,7 @@ def main():
                                        else "1 GPU")},
             "latency_p50_ms": float(np.median(lat)) if lat.size else None,
             "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
-            "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"},
+            "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
             "roofline": rf,
             "cpu_baseline": cpu,
             "cpu_baseline_all": cpu_all,
@@ -400,9 +405,9 @@ def main():
                 "rccl_nranks": r["nranks"], "collective": (
                     "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
                     if r["native"] else "torch.distributed all_reduce(SUM) of the slots"),
-                "allreduce_us": tim.get("allreduce_us"),
+                "allreduce_us": tim.get("allreduce_us") if tim else None,
                 "native_comm_error": r["native_error"],
-                "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks"),
+                "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
                 "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
         print(json.dumps(line), flush=True)
     if dist is not None:

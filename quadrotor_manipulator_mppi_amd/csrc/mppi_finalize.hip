@@ -26,7 +26,8 @@ using namespace mppi;
 constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 waves)
 constexpr int kMaxRec = 4096;
 // timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
-// outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor)
+// outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor), 32 skips
+// the u_prev update
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
@@ -252,7 +253,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const float un = u_old + sm;
     if (own) {
         if (wsmooth) wsmooth[((size_t)v * H + t) * A + a] = sm;
-        up[t * A + a] = un;
+        if (!(MPPI_FIN_KO & 32)) up[t * A + a] = un;   // (32: timing knockout, u_prev not written)
     }
     if (!(MPPI_FIN_KO & 2) && sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
 #pragma clang fp contract(off)

@@ -22,7 +22,8 @@
 
 // Timing knockouts for tools/ experiments only (MPPI_HIPCC_EXTRA=-DMPPI_KO=n; results are
 // wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain,
-// 8 the pose cost, 16 the trajectory stores, 32 Box-Muller, 64 the block record body.
+// 8 the pose cost, 16 the trajectory stores, 32 Box-Muller, 64 the block record body,
+// 128 the u_prev loads (H*A <= 4 * block threads).
 #ifndef MPPI_KO
 #define MPPI_KO 0
 #endif
@@ -623,7 +624,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i = tid + j * nthr;
-        ur[j] = (i < HA) ? usrc[i] : 0.0f;
+        ur[j] = (i < HA && !(MPPI_KO & 128)) ? usrc[i] : 0.0f;
     }
     if (MODEL != MPPI_MODEL_DRONE) {
         const int* js = (const int*)jtab;
