@@ -521,14 +521,10 @@ __device__ __forceinline__ float row_shr_f32(float x) {   // out-of-row sources 
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
 }
 
-// inc[a] (lane = segment*L + t) = q(t) - q0 for the controls act[a] of this lane.
-// fill1 / fill2 run while the transposed reads and the increments' reads are in flight
-// (independent VALU work of the caller: the next rollout group's noise draw).
-struct NoFill { __device__ void operator()() const {} };
-template <int L, int NA, typename F1 = NoFill, typename F2 = NoFill>
+// inc[a] (lane = segment*L + t) = q(t) - q0 for the controls act[a] of this lane
+template <int L, int NA>
 __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw, const int lane, const float dt,
-                                              const float dt2h, const float* vel0f, float (&inc)[NA],
-                                              F1&& fill1 = NoFill(), F2&& fill2 = NoFill()) {
+                                              const float dt2h, const float* vel0f, float (&inc)[NA]) {
     using G = IntegGeom<L, NA>;
     constexpr int P = G::P, CPS = G::CPS, CL = G::CL, S = G::S;
 #pragma unroll
@@ -538,13 +534,10 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     const bool on = sr < S;
     const int seg = sr / NA, a = sr - seg * NA;
     const int rb = on ? (seg * L + ch * CL) * P + a : 0;
-    float lv = 0.0f, lp = 0.0f, loc[CL], xin[CL];
-#pragma unroll
-    for (int i = 0; i < CL; ++i) xin[i] = xw[rb + i * P];
-    fill1();
+    float lv = 0.0f, lp = 0.0f, loc[CL];
 #pragma unroll
     for (int i = 0; i < CL; ++i) {
-        const float x = xin[i];
+        const float x = xw[rb + i * P];
         lp += fmaf(lv, dt, x * dt2h);
         lv = fmaf(x, dt, lv);
         loc[i] = lp;
@@ -570,7 +563,6 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     wave_lds_handoff();
 #pragma unroll
     for (int a2 = 0; a2 < NA; ++a2) inc[a2] = xw[lane * P + a2];
-    fill2();
 }
 
 // The leading scalar arguments are preloaded into SGPRs at wave launch on gfx950
@@ -594,13 +586,6 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
     constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
     constexpr int NQ = (MODEL == MPPI_MODEL_DRONE) ? 0 : NA - QOFF;
     constexpr int kJW = (int)(sizeof(JointDev) * kMaxJ / 4);   // joint table, dwords
-    // looping kernel, one chunk: group it + 1's normals are drawn inside group it's
-    // integrator, whose LDS round trips otherwise leave the SIMD idle (the 4 waves of a
-    // SIMD reach them together); MPPI_PIPE=0 draws them at the start of each group
-#ifndef MPPI_PIPE
-#define MPPI_PIPE 1
-#endif
-    constexpr bool kPipe = MPPI_PIPE && NCH == 1 && !ONEG && !(MPPI_KO & 1);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // Scalars and (V == 1) the vehicle constants are read from the kernel
     // arguments with scalar loads (SGPR operands, no LDS latency in the hot
@@ -728,7 +713,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
                 for (int a = 0; a < NA; ++a) eps[c][a] = src[a];
             } else {
                 float z[NA];
-                if (it == 0 || kPipe) {   // drawn in the prologue / during the previous group
+                if (it == 0) {
 #pragma unroll
                     for (int a = 0; a < NA; ++a) z[a] = z0[c][a];
                 } else {
@@ -812,19 +797,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rol
         double posd[NCH][F64 ? NA : 1];
         if constexpr (NCH == 1 && !(MPPI_KO & 1)) {
             float inc[NA];
-            // the next group's normals fill the integrator's two LDS round trips (kPipe)
-            const bool pipe = kPipe && noise_mode != MPPI_NOISE_INJECTED && it + 1 < p.iters;
-            uint32_t wn[draw_words<NA>()];
-            auto fill1 = [&]() {
-                if (pipe) {
-                    const uint32_t kgn = k_off + (uint32_t)(((blockIdx.x + (it + 1) * p.nb) * nw + wid) * R + sub);
-                    draw_philox<NA>(wn, kgn, (uint32_t)t0, (uint32_t)v, step_ctr, seed_lo, seed_hi);
-                }
-            };
-            auto fill2 = [&]() {
-                if (pipe) draw_box_muller<NA>(wn, z0[0]);
-            };
-            integrate_lds<LSEG, NA>(act[0], xw, lane, p.dt, 0.5f * p.dt2, vc.vel0f, inc, fill1, fill2);
+            integrate_lds<LSEG, NA>(act[0], xw, lane, p.dt, 0.5f * p.dt2, vc.vel0f, inc);
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 if (!F64) {
