@@ -31,6 +31,10 @@ constexpr int kMaxRec = 4096;
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
+// XCDs the finalize's blocks run on (8; 4 = the first four, see the block map in k_finalize)
+#ifndef MPPI_FIN_XCDS
+#define MPPI_FIN_XCDS 8
+#endif
 
 #ifdef MPPI_STAMPS
 #define FSTAMP(i)                                                                    \
@@ -75,13 +79,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
     const int tsz = (int)(geo & 0xFFu), hf = (int)((geo >> 8) & 0xFFu), ts = (int)((geo >> 16) & 0xFFu);
     const int A = (int)(geo >> 24);
-    // XCD-aware block map: the dispatcher deals blocks round robin over the 8 XCDs, so
-    // block b = a + Ga*sl (Ga = A rounded up to 8) puts every slice of dim a on XCD a mod 8:
-    // the slices read the same record lines (one 128 B line holds 32 t of a row), which one
-    // L2 then fetches once instead of once per slice.  Blocks with a >= A exit at once.
-    const int Ga = (A + 7) & ~7;
-    const int sl = blockIdx.x / Ga, a = blockIdx.x - sl * Ga, v = blockIdx.y;
-    if (a >= A) return;
+    // XCD-aware block map: the dispatcher deals blocks round robin over the 8 XCDs (block b
+    // on XCD b mod 8).  Dim a lives on XCD a mod X (X = MPPI_FIN_XCDS of them), every slice of
+    // it too: the slices read the same record lines (one 128 B line holds 32 t of a row),
+    // which one L2 then fetches once instead of once per slice.  Blocks b mod 8 >= X and
+    // dims >= A exit at once.
+    const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3, na = (A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS;
+    const int sl = j8 / na, a = x8 + MPPI_FIN_XCDS * (j8 - sl * na), v = blockIdx.y;
+    if (x8 >= MPPI_FIN_XCDS || a >= A) return;
     if (MPPI_FIN_KO & 16) { if (tid == 0) u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
     FSTAMP(0);
     const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
@@ -323,7 +328,7 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     int nt = 512;
     for (int c : {128, 256})
         if (c * 16 / cw >= p->nrec) { nt = c; break; }
-    const dim3 grid(((p->A + 7) & ~7) * p->ts, p->V), block(nt);   // XCD-aware map (k_finalize)
+    const dim3 grid(8 * ((p->A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS) * p->ts, p->V), block(nt);   // XCD-aware map (k_finalize)
     hipStream_t s = (hipStream_t)stream;
 #define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
     hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo, \
