@@ -434,13 +434,20 @@ __device__ __forceinline__ void traj_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
     if (MPPI_KO & 16) return;
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)voff, (int)soff, MPPI_TRAJ_AUX);
 }
-// The same policy for the record bodies the finalize reads (full 256 B t-runs): a raw
+// Write-through stores for the record bodies the finalize reads (full 256 B t-runs): a raw
 // buffer over a wave-uniform base, byte offsets < 4 GiB.  NOT for S: its one-lane 4 B
 // stores become partial-line writes through to memory (whole-body K=8192 rollout
 // 13.7 -> 19.0 us, profiles/r02/ab_store_policy.txt); in L2 they merge into full lines.
+// Record bodies: sc1 (written through) without nt, so the lines stay allocated on their way
+// to memory and the finalize's loads (other XCDs) come back sooner.  Order-balanced A/B vs
+// sc1|nt (profiles/r02/ab_record_store_policy.txt): step pair arm C3 10.40 -> 10.08 us,
+// whole-body K=8192 19.66 -> 18.96 us, quadrotor 12.25 -> 11.99 us.
+#ifndef MPPI_REC_AUX
+#define MPPI_REC_AUX 16
+#endif
 __device__ __forceinline__ void wt_store(float* base_uniform, uint32_t byte_off, float x) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base_uniform, 0, (int)0xFFFFFFFFu, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)byte_off, 0, MPPI_TRAJ_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)byte_off, 0, MPPI_REC_AUX);
 }
 
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
