@@ -256,16 +256,16 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
     dt = time.perf_counter() - t0
     tim = None
     if timing:   # per-kernel HIP-event timing in its own region (events perturb the step rate)
-        n_t = max(50, steps_n // 5)
+        n_t = max(200, steps_n // 5)
         # n launches of each kernel back to back between one event pair, then n (rollout,
-        # finalize) pairs as a step runs them; median of 5 batches (a transient clock dip on
+        # finalize) pairs as a step runs them; median of 7 batches (a transient clock dip on
         # the box moves one batch, not the median)
-        rs, fs, ps = zip(*[eng.kernel_timing_ex(n_t) for _ in range(5)])
+        rs, fs, ps = zip(*[eng.kernel_timing_ex(n_t) for _ in range(7)])
         r_us, f_us, p_us = float(np.median(rs)), float(np.median(fs)), float(np.median(ps))
         tim = {"rollout_us": r_us, "finalize_us": f_us, "pair_us": p_us,
                "rollout_in_step_us": max(r_us, p_us - f_us),
                "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
-                         f"median of 5 batches, on the engine stream",
+                         f"median of 7 batches, on the engine stream",
                "rollout_us_batches": [round(x, 3) for x in rs]}
         if se.native and world > 1:   # the step's one collective alone (collective call on every rank)
             tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
