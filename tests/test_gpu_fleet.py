@@ -82,7 +82,7 @@ def _check_reduction(S_gpu, raw, sm, u_prev_gpu, ref, noise, window, what):
     return float(sm_bound.max()) + 1e-6
 
 
-def _fleet_inputs(V, K, H, seed):
+def _fleet_inputs(V, K, H, seed, sigma=WB_SIGMA):
     """C4 state + U(-0.5,0.5) m xyz and U(-0.2,0.2) rad joint offsets,
     targets jittered by +-0.1 m; here also a per-vehicle base yaw, base/joint rates and
     warm start so that every per-vehicle input of the launch differs."""
@@ -98,18 +98,18 @@ def _fleet_inputs(V, K, H, seed):
         qd = rng.uniform(-0.4, 0.4, 7).tolist()
         tpos = (np.array(ARM_TARGET[0]) + rng.uniform(-0.1, 0.1, 3)).astype(np.float32)
         u_prev = (torch.randn(H, 10) * torch.tensor([2.0] * 3 + [0.2] * 7)).float()
-        noise = O.draw_noise(K, H, torch.from_numpy(WB_SIGMA))
+        noise = O.draw_noise(K, H, torch.from_numpy(sigma))
         # the engine's state vector: base pos(3) quat(4) q(7) base vel(3) qd(7)
         state = np.array(x + quat + q + vx + qd, np.float64)
         veh.append(dict(x=x, quat=quat, q=q, vx=vx, qd=qd, tpos=tpos, u_prev=u_prev, noise=noise, state=state))
     return veh
 
 
-def _run_fleet_vs_oracle(V, K, H):
+def _run_fleet_vs_oracle(V, K, H, sigma=WB_SIGMA):
     chain = _chain()
-    veh = _fleet_inputs(V, K, H, seed=1000 + V + H)
+    veh = _fleet_inputs(V, K, H, seed=1000 + V + H, sigma=sigma)
     e = _engine(model="wholebody", n_samples=K, n_horizon=H, n_vehicles=V, noise="injected",
-                sigma=WB_SIGMA)
+                sigma=sigma)
     for v, d in enumerate(veh):
         e.set_target(d["tpos"], ARM_TARGET[1], vehicle=v)
     e.set_u_prev(np.stack([d["u_prev"].numpy() for d in veh]))
@@ -147,6 +147,17 @@ def test_fleet_long_horizon_matches_oracle():
     """V=3 at H=128 (NCH = 2: DPP segment scans with a carry between the 64-step
     chunks) -- the batched path on the long-horizon lane map."""
     _run_fleet_vs_oracle(3, 256, 128)
+
+
+@pytest.mark.parametrize("V", [1, 3])
+def test_wholebody_full_sigma_extended_kernel(V):
+    """A non-diagonal Sigma runs the whole-body rollout in the extended (XC) instantiation
+    (its own register budget, the full z Sigma product): every vehicle against the oracle
+    on the same injected noise, V == 1 (constants in the kernel arguments) and V > 1."""
+    sig = WB_SIGMA.astype(np.float64).copy()
+    sig[0, 1] = sig[1, 0] = 2.0          # xy correlation of the drone dims
+    sig[4, 5] = sig[5, 4] = 0.02         # two arm joints
+    _run_fleet_vs_oracle(V, 256, 64, sigma=sig.astype(np.float32))
 
 
 def test_fleet_c5_full_size_properties():
