@@ -1341,6 +1341,43 @@ done:
     return st;
 }
 
+#ifdef MPPI_PROBE
+// tools-only (MPPI_PROBE builds): average time of n repetitions of a kernel sequence
+//   mode 0: rollout, empty kernel   1: rollout, rollout of one block   2: rollout, finalize
+//   3: empty kernel                 4: rollout of one block            5: rollout
+extern "C" int mppi_launch_boundary(float* scratch, int blocks, void* stream);
+extern "C" mppi_status mppi_probe_sequence(mppi_engine* e, int32_t n, int32_t mode, double* us) {
+    if (use_device(e)) return MPPI_ERR_HIP;
+    DevParams p = e->dp;
+    p.vc0 = e->h_vc[0];
+    p.step_ctr = e->step_ctr;
+    DevParams p1 = p;
+    p1.nb = 1;
+    FinParams f = e->fp;
+    f.mode = 0; f.seq = 0u;
+    final_records(e, f);
+    f.out = (double*)e->d_out; f.u0 = (float*)(e->d_out + off_u0(e)); f.stats = (float*)(e->d_out + off_stats(e));
+    f.flags = (uint32_t*)(e->d_out + off_flags(e)); f.wraw = nullptr; f.wsmooth = nullptr;
+    const int fb = 8 * ((e->A + 7) / 8) * ((e->H + 7) / 8) * e->V;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, e->stream);
+    for (int i = 0; i < n; ++i) {
+        if (mode <= 2 || mode == 5) mppi_launch_rollout(&p, e->threads, e->stream);
+        if (mode == 0 || mode == 3) mppi_launch_boundary((float*)e->d_out, fb, e->stream);
+        if (mode == 1 || mode == 4) mppi_launch_rollout(&p1, e->threads, e->stream);
+        if (mode == 2) mppi_launch_finalize(&f, e->stream);
+    }
+    (void)hipEventRecord(b, e->stream);
+    (void)hipEventSynchronize(b);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    *us = 1e3 * ms / n;
+    (void)hipEventDestroy(a); (void)hipEventDestroy(b);
+    return MPPI_OK;
+}
+#endif
+
 mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
     return mppi_kernel_timing_ex(e, n, rollout_us, finalize_us, nullptr);
 }

@@ -354,6 +354,16 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     return (int)hipGetLastError();
 }
 
+#ifdef MPPI_PROBE
+__global__ void __launch_bounds__(256) k_boundary(float* scratch) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) scratch[0] = 0.0f;
+}
+extern "C" int mppi_launch_boundary(float* scratch, int blocks, void* stream) {
+    hipLaunchKernelGGL(k_boundary, dim3(blocks), dim3(256), 0, (hipStream_t)stream, scratch);
+    return (int)hipGetLastError();
+}
+#endif
+
 extern "C" int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int K, float coef,
                                    void* stream) {
     const int n = V * K;
