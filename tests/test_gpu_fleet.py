@@ -268,3 +268,39 @@ def test_output_sequence_survives_step_counter_rewind():
     assert np.array_equal(u02[0], up[0]), "u0 must be the replayed step's u_prev[0]"
     assert not np.array_equal(u01, u02), "the replay moved u_prev, so u0 must differ"
     e.close()
+
+
+# ------------------------------------------ SavGol windows (finalize template / generic path)
+@pytest.mark.parametrize("model,H,window,order", [("arm", 32, 7, 3), ("arm", 16, 11, 2), ("arm", 32, 3, 1),
+                                                  ("drone", 20, 9, 2), ("drone", 64, 13, 4),
+                                                  ("wholebody", 64, 5, 2)])
+def test_savgol_windows_match_oracle(model, H, window, order):
+    """The finalize's SavGol for every window class: the templated 9- and 5-tap kernels
+    and the generic one (3, 7, 11, 13 taps), at horizons whose slices put the reflected
+    pads (svg_filter.py:58) inside the window; checked as the reference filter of the
+    device's own raw weighted noise (rtol 1e-5), and the update u += SavGol(w_eps)."""
+    A = {"arm": 7, "drone": 3, "wholebody": 10}[model]
+    K = 512
+    torch.manual_seed(window * 31 + H)
+    rng = np.random.default_rng(window)
+    sig = np.eye(A, dtype=np.float32) * 0.2
+    noise = O.draw_noise(K, H, torch.from_numpy(sig)).numpy()
+    u_prev = rng.normal(0, 0.3, (H, A)).astype(np.float32)
+    e = _engine(model=model, n_samples=K, n_horizon=H, noise="injected", sigma=sig, savgol_window=window,
+                savgol_order=order)
+    if model == "drone":
+        e.set_target(np.asarray([0.5, 0.4, 2.0], np.float32))
+        state = np.array([0.0, 0.0, 1.0, 0.1, -0.1, 0.0], np.float64)
+    else:
+        e.set_target(*ARM_TARGET)
+        state = (np.array([0, 0, 1, 0, 0, 0, 1] + HOME_Q + [0.0] * 7, np.float64) if model == "arm" else
+                 np.array([0, 0, 1, 0, 0, 0, 1] + HOME_Q + [0.0] * 10, np.float64))
+    e.set_u_prev(u_prev)
+    e.step(state, noise[None])
+    raw, sm = e.get_weighted_noise()
+    up = e.get_u_prev()[0]
+    e.close()
+    want = O.savgol(torch.from_numpy(raw[0].astype(np.float32)), window, order).numpy()
+    scale = float(np.abs(raw[0]).max())
+    _close(sm[0], want, rtol=1e-5, atol=1e-6 * scale, what=f"{model} H={H} savgol({window},{order})")
+    _close(up, u_prev + sm[0], rtol=1e-6, atol=1e-7, what="u_prev += w_eps")
