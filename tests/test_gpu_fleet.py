@@ -160,6 +160,13 @@ def test_wholebody_full_sigma_extended_kernel(V):
     _run_fleet_vs_oracle(V, 256, 64, sigma=sig.astype(np.float32))
 
 
+def test_wholebody_ragged_k_looping_kernel():
+    """K = 2999 on V = 2 vehicles runs the looping kernel (125 blocks x 3 groups of 8 waves per
+    vehicle = 3000 rollout slots): the padding rollout of the last group must stay out of
+    every vehicle's trajectory, S, records and weights."""
+    _run_fleet_vs_oracle(2, 2999, 64)
+
+
 def test_fleet_c5_full_size_properties():
     """C5 per-GPU share at full size: V=8 x K=8192 x H=64 whole-body with device Philox.
     Per vehicle: finite costs, sum w = 1, w_eps = sum_k w_k eps_k of the stored noise;
