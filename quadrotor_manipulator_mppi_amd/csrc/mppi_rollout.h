@@ -28,6 +28,13 @@
 #define MPPI_KO 0
 #endif
 // waves per SIMD the rollout kernel is register-budgeted for (4: <= 128 VGPRs)
+// NCH == 4 (H in 193..256) is budgeted for 2 waves (<= 256 VGPRs): at 4 it spilled
+// 0.3-2 KB per lane and ran 2.3x slower (arm K=4096 H=256 40.7 -> 28.1 us, whole-body
+// 81.8 -> 35.3 us); NCH == 2 keeps 4 (its 8-96 B spill is cheaper than 3 or 2 waves:
+// arm H=128 13.6 us at 4, 16.7 at 3 and 2; profiles/r02/ab_rollout_occupancy_long_h.txt)
+#ifndef MPPI_ROLL_OCC_NCH2
+#define MPPI_ROLL_OCC_NCH2 4
+#endif
 #ifndef MPPI_ROLL_OCC
 #define MPPI_ROLL_OCC 4
 #endif
@@ -583,7 +590,7 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
 // (whole-body K=8192 H=64) that is 1024 blocks x 8 waves, all resident at once: twice the
 // latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
-__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : MPPI_ROLL_OCC) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? MPPI_ROLL_OCC_NCH2 : MPPI_ROLL_OCC)) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
                                                  const int32_t nthr,
