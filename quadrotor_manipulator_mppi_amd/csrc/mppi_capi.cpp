@@ -353,6 +353,20 @@ namespace {
 // communicator (a one-rank communicator runs the same pack -> all-reduce -> combine)
 bool sharded(const mppi_engine* e) { return e->cfg.shard_count > 1 || e->comm; }
 
+// Trajectory planes: k_rollout rows (one rollout's H steps) are padded to 64 B, hp = H
+// rounded up to 16 floats, and written whole.  With H = 100 the unpadded rows left partial
+// 64 B sectors at both ends of every wave store, which the write-through stores hand to HBM
+// as masked writes: arm K=4096 rollout 20.3 us at H = 100 vs 13.4 at H = 128
+// (profiles/r02/ab_traj_row_pitch.txt).  k_rollout_quad writes t-major (C,H,K) planes.
+int traj_pitch(const mppi_engine* e) {
+    return e->cfg.model == MPPI_MODEL_QUADROTOR ? e->K : (e->H + 15) & ~15;
+}
+size_t traj_floats(const mppi_engine* e) {   // all vehicles' planes
+    const size_t plane = e->cfg.model == MPPI_MODEL_QUADROTOR ? (size_t)e->K * e->H
+                                                               : (size_t)e->K * traj_pitch(e);
+    return (size_t)e->V * e->C * plane;
+}
+
 mppi_status use_device(mppi_engine* e) {
     HIP_TRY(hipSetDevice(e->cfg.device));
     return MPPI_OK;
@@ -716,7 +730,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     const int P = (kHdr + e->A * H + 3) & ~3;
     // the rollout kernels address one vehicle's trajectory planes through a buffer
     // resource (32-bit byte offsets) and the record bodies with 32-bit indices
-    if (c.store_trajectory && (uint64_t)e->C * e->K * H * sizeof(float) > 0xFFFFFFFFull) {
+    if (c.store_trajectory && (uint64_t)e->C * e->K * ((H + 15) & ~15) * sizeof(float) > 0xFFFFFFFFull) {
         const int C = e->C, K = e->K;
         delete e;
         return fail(MPPI_ERR_INVALID_ARG, "trajectory of one vehicle (C=%d x K=%d x H=%d floats) exceeds 4 GiB: "
@@ -759,7 +773,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_rdata, sizeof(float) * (size_t)e->V * e->A * nb * H));
     CREATE_TRY(hipMalloc(&e->d_wraw, sizeof(float) * e->V * H * e->A));
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
-    if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * KH * e->C));
+    if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * traj_floats(e)));
     if (c.store_noise) CREATE_TRY(hipMalloc(&e->d_noise_out, sizeof(float) * KH * e->A));
     e->out_bytes = (int64_t)(off_flags(e) + (size_t)e->V * e->A * sizeof(uint32_t));
     CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
@@ -854,7 +868,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
             if (kin && !getenv("MPPI_NO_KINOVA_PATH")) p.chain_fast = 2;
         }
     }
-    p.P = P; p.C = e->C;
+    p.P = P; p.C = e->C; p.hp = traj_pitch(e);
     p.seed_lo = (uint32_t)c.seed; p.seed_hi = (uint32_t)(c.seed >> 32);
     p.k_offset = (int64_t)c.shard_rank * e->K;
     p.dt = (float)c.dt; p.dt2 = (float)(c.dt * c.dt); p.dt_d = c.dt;
@@ -1444,7 +1458,8 @@ mppi_status mppi_get_trajectory(mppi_engine* e, float* traj) {
     if (!e || !traj) return fail(MPPI_ERR_INVALID_ARG, "null argument");
     if (!e->d_traj) return fail(MPPI_ERR_STATE, "engine created without store_trajectory");
     if (use_device(e)) return MPPI_ERR_HIP;
-    const size_t KH = (size_t)e->K * e->H, n = (size_t)e->V * e->C * KH;
+    const size_t KH = (size_t)e->K * e->H, n = traj_floats(e);
+    const size_t hp = (size_t)traj_pitch(e), plane = n / ((size_t)e->V * e->C);   // padded plane
     std::vector<float> soa(n);
     HIP_TRY(hipMemcpyAsync(soa.data(), e->d_traj, n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1455,12 +1470,12 @@ mppi_status mppi_get_trajectory(mppi_engine* e, float* traj) {
     for (int v = 0; v < e->V; ++v)
         for (size_t i = 0; i < KH; ++i) {
             float* dst = traj + ((size_t)v * KH + i) * Cr;
-            const size_t ii = t_major ? (i % e->H) * e->K + i / e->H : i;
-            const float* src = soa.data() + (size_t)v * e->C * KH + ii;
-            for (int c = 0; c < nstate; ++c) dst[c] = src[c * KH];
+            const size_t ii = t_major ? (i % e->H) * e->K + i / e->H : (i / e->H) * hp + i % e->H;
+            const float* src = soa.data() + (size_t)v * e->C * plane + ii;
+            for (int c = 0; c < nstate; ++c) dst[c] = src[c * plane];
             if (has_ee) {
                 float* ee = dst + nstate;
-                for (int r = 0; r < 12; ++r) ee[r] = src[(nstate + r) * KH];
+                for (int r = 0; r < 12; ++r) ee[r] = src[(nstate + r) * plane];
                 ee[12] = 0.0f; ee[13] = 0.0f; ee[14] = 0.0f; ee[15] = 1.0f;
             }
         }

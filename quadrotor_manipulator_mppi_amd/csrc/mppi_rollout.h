@@ -692,8 +692,11 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
 
     // trajectory planes of vehicle v (from kernel arguments and blockIdx only, so the
     // descriptor stays in SGPRs)
-    const uint32_t plane_b = (uint32_t)K * (uint32_t)H * 4u;
-    const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * K * H, plane_b, pk.C);
+    // rows padded to 64 B (hp = H rounded up to 16) and written whole, pad lanes included: the
+    // write-through stores then never leave a partial 64 B sector for HBM to merge
+    const int hp = pk.hp;
+    const uint32_t plane_b = (uint32_t)K * (uint32_t)hp * 4u;
+    const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * K * hp, plane_b, pk.C);
 
     float acc[NCH][NA];
 #pragma unroll
@@ -889,12 +892,13 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             const bool val = kval && t < H;
             const bool term = (t == H - 1);
             float x;
-            const uint32_t toff = ((uint32_t)k * (uint32_t)H + (uint32_t)t) * 4u;   // byte offset in a plane
+            const uint32_t toff = ((uint32_t)k * (uint32_t)hp + (uint32_t)t) * 4u;   // byte offset in a plane
+            const bool stv = p.store_traj && kval && t < hp;   // row incl. its pad (finite values)
             if (MODEL == MPPI_MODEL_DRONE) {
                 const float dx = posf[c][0] - vc.tpos[0], dy = posf[c][1] - vc.tpos[1],
                             dz = posf[c][2] - vc.tpos[2];
                 x = dx * dx + dy * dy + dz * dz;
-                if (p.store_traj && val) {
+                if (stv) {
 #pragma unroll
                     for (int a = 0; a < 3; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
                 }
@@ -903,7 +907,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
                 auto qang = [&](int cc_, int j) {
                     if constexpr (F64) return posd[cc_][QOFF + j]; else return posf[cc_][QOFF + j];
                 };
-                if (p.store_traj && val) {   // positions first: each dies after its joint's FK step
+                if (stv) {   // positions first: each dies after its joint's FK step
 #pragma unroll
                     for (int a = 0; a < NA; ++a) traj_store(trs, toff, (uint32_t)a * plane_b, posf[c][a]);
                 }
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
                 const float wsp = uniform_f32(p.w_sp), wso = uniform_f32(p.w_so), wtp = uniform_f32(p.w_tp),
                             wto = uniform_f32(p.w_to);
                 x = (MPPI_KO & 8) ? T.m[3] + T.m[7] + T.m[11] + T.m[0] : pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
-                if (p.store_traj && val) {
+                if (stv) {
 #pragma unroll
                     for (int i = 0; i < 12; ++i) traj_store(trs, toff, (uint32_t)(NA + i) * plane_b, T.m[i]);
                 }
