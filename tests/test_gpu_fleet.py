@@ -209,10 +209,11 @@ def test_fleet_c5_full_size_properties():
 
 
 # ------------------------------------------------------------ long horizons (H > 64)
-@pytest.mark.parametrize("H,f64", [(100, True), (128, False), (128, True)])
+@pytest.mark.parametrize("H,f64", [(65, True), (100, True), (128, False), (128, True), (200, True), (256, False)])
 def test_arm_long_horizons_match_oracle(H, f64):
-    """Arm at H = 100 / 128 (NCH = 2 DPP-scan integrator, fp32 and fp64 state) against
-    the oracle: trajectory, EE, S and the update (standard_normal_noise.py:41-48)."""
+    """Arm at H = 65..256 (NCH = 2 and 4 DPP-scan integrator, fp32 and fp64 state; NCH = 4
+    runs the 2-wave register budget; H = 65 / 100 / 200 pad the trajectory rows to 64 B)
+    against the oracle: trajectory, EE, S and the update (standard_normal_noise.py:41-48)."""
     chain = _chain()
     K = 256
     torch.manual_seed(300 + H)
@@ -234,9 +235,9 @@ def test_arm_long_horizons_match_oracle(H, f64):
     _check_reduction(S, raw[0], sm[0], e.get_u_prev()[0], r, noise.numpy(), 9, f"arm H={H}")
 
 
-@pytest.mark.parametrize("H", [100, 128])
+@pytest.mark.parametrize("H", [65, 100, 128, 200])
 def test_wholebody_long_horizons_match_oracle(H):
-    """Whole-body at H = 100 / 128 against the oracle's composed step (A16)."""
+    """Whole-body at H = 65..200 (NCH = 2 and 4) against the oracle's composed step (A16)."""
     chain = _chain()
     K = 256
     torch.manual_seed(400 + H)

@@ -202,8 +202,10 @@ def test_wholebody_matches_composed_fixture():
 
 
 # ------------------------------------------------------------- horizon chunks H>64
-@pytest.mark.parametrize("H", [20, 64, 100, 128])
+@pytest.mark.parametrize("H", [20, 64, 100, 128, 200, 256])
 def test_drone_horizons_match_oracle(H):
+    """Drone horizons over every lane map: L = 32, 64, NCH = 2 and NCH = 4 (H = 193..256,
+    the 2-wave register budget), rows padded to 64 B (H = 20, 100, 200)."""
     K = 512
     torch.manual_seed(H)
     noise = O.draw_noise(K, H, torch.eye(3) * 30.0)
