@@ -357,12 +357,13 @@ bool sharded(const mppi_engine* e) { return e->cfg.shard_count > 1 || e->comm; }
 // rounded up to 16 floats, and written whole.  With H = 100 the unpadded rows left partial
 // 64 B sectors at both ends of every wave store, which the write-through stores hand to HBM
 // as masked writes: arm K=4096 rollout 20.3 us at H = 100 vs 13.4 at H = 128
-// (profiles/r02/ab_traj_row_pitch.txt).  k_rollout_quad writes t-major (C,H,K) planes.
+// (profiles/r02/ab_traj_row_pitch.txt).  k_rollout_quad writes t-major (C,H,Kp) planes,
+// its rows (one step's K samples) padded the same way: Kp = K rounded up to 16.
 int traj_pitch(const mppi_engine* e) {
-    return e->cfg.model == MPPI_MODEL_QUADROTOR ? e->K : (e->H + 15) & ~15;
+    return e->cfg.model == MPPI_MODEL_QUADROTOR ? (e->K + 15) & ~15 : (e->H + 15) & ~15;
 }
 size_t traj_floats(const mppi_engine* e) {   // all vehicles' planes
-    const size_t plane = e->cfg.model == MPPI_MODEL_QUADROTOR ? (size_t)e->K * e->H
+    const size_t plane = e->cfg.model == MPPI_MODEL_QUADROTOR ? (size_t)traj_pitch(e) * e->H
                                                                : (size_t)e->K * traj_pitch(e);
     return (size_t)e->V * e->C * plane;
 }
@@ -730,7 +731,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     const int P = (kHdr + e->A * H + 3) & ~3;
     // the rollout kernels address one vehicle's trajectory planes through a buffer
     // resource (32-bit byte offsets) and the record bodies with 32-bit indices
-    if (c.store_trajectory && (uint64_t)e->C * e->K * ((H + 15) & ~15) * sizeof(float) > 0xFFFFFFFFull) {
+    if (c.store_trajectory && (uint64_t)e->C * ((e->K + 15) & ~15) * ((H + 15) & ~15) * sizeof(float) > 0xFFFFFFFFull) {
         const int C = e->C, K = e->K;
         delete e;
         return fail(MPPI_ERR_INVALID_ARG, "trajectory of one vehicle (C=%d x K=%d x H=%d floats) exceeds 4 GiB: "
@@ -1470,7 +1471,7 @@ mppi_status mppi_get_trajectory(mppi_engine* e, float* traj) {
     for (int v = 0; v < e->V; ++v)
         for (size_t i = 0; i < KH; ++i) {
             float* dst = traj + ((size_t)v * KH + i) * Cr;
-            const size_t ii = t_major ? (i % e->H) * e->K + i / e->H : (i / e->H) * hp + i % e->H;
+            const size_t ii = t_major ? (i % e->H) * hp + i / e->H : (i / e->H) * hp + i % e->H;
             const float* src = soa.data() + (size_t)v * e->C * plane + ii;
             for (int c = 0; c < nstate; ++c) dst[c] = src[c * plane];
             if (has_ee) {

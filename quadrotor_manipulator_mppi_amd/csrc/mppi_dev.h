@@ -78,7 +78,8 @@ struct DevParams {
                         // 2: additionally the Kinova origin table kKinova
     int32_t P;          // floats per partial record (kHdr + A*H, rounded up to 4)
     int32_t C;          // stored trajectory channels (EE as 12)
-    int32_t hp;         // trajectory row pitch in floats: H rounded up to 16 (k_rollout; 64 B rows)
+    int32_t hp;         // trajectory row pitch in floats, 64 B rows: H rounded up to 16 (k_rollout),
+                        // K rounded up to 16 (k_rollout_quad, t-major planes)
     uint32_t seed_lo, seed_hi;
     int64_t k_offset;   // global index of this shard's first sample
     float dt, dt2;      // fp32(dt), fp32(dt**2)
@@ -95,7 +96,7 @@ struct DevParams {
     const float* u_prev;     // (V,H,A)
     const float* noise_in;   // (V,K,H,A) injected
     uint32_t step_ctr;       // control-step index: the Philox counter word (host-counted)
-    float* traj;             // (V,C,K,hp) SoA planes (QUADROTOR: (V,C,H,K))
+    float* traj;             // (V,C,K,hp) SoA planes (QUADROTOR: (V,C,H,hp))
     float* noise_out;        // (V,K,H,A)
     float* S;                // (V,K)
     float* hdr;              // (V,nb,4) partial record headers: rho, eta, eta2, nan

@@ -169,12 +169,15 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
     // this lane's axis of the state: position, Euler angle, world velocity, body rate
     float pj = axis(x6), ej = axis(x6 + 3), vj = axis(v6), wj = axis(v6 + 3);
     const float ox0 = v6[3], oy0 = v6[4], oz0 = v6[5];   // measured body rates
-    // trajectory planes t-major, (V, C, H, K): lane (r, j) writes channel j (position) and
-    // 3 + j (angle) of sample k; a store instruction covers 16 consecutive k of 3 planes
-    const uint32_t plane_b = (uint32_t)K * (uint32_t)H * 4u;
-    const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * K * H, plane_b, pk.C);
-    const uint32_t off_p = (uint32_t)kc * 4u + (uint32_t)jj * plane_b, off_e = off_p + 3u * plane_b;
-    const uint32_t tstep_b = (uint32_t)K * 4u;
+    // trajectory planes t-major, (V, C, H, Kp): lane (r, j) writes channel j (position) and
+    // 3 + j (angle) of sample k; a store instruction covers 16 consecutive k (64 B) of 3
+    // planes.  Rows are padded to Kp = K rounded up to 16 (pk.hp) and the lanes past K write
+    // the pad (sample K-1's values), so a ragged K leaves no partial 64 B sector
+    const int kp = pk.hp;
+    const uint32_t plane_b = (uint32_t)kp * (uint32_t)H * 4u;
+    const __amdgpu_buffer_rsrc_t trs = traj_rsrc(pk.traj + (size_t)v * pk.C * kp * H, plane_b, pk.C);
+    const uint32_t off_p = (uint32_t)(k < kp ? k : kc) * 4u + (uint32_t)jj * plane_b, off_e = off_p + 3u * plane_b;
+    const uint32_t tstep_b = (uint32_t)kp * 4u;
     const bool store = sstore != 0;
     float stage = 0.0f, term = 0.0f;
     const float a0 = (j == 0) ? 1.0f : 0.0f;   // J's column 0 is (1, 0, 0)
