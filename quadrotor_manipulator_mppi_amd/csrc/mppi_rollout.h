@@ -709,7 +709,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // One group of R rollouts per wave.  Written as a lambda so the common
     // single-group launch (iters == 1, e.g. K=4096 H=32) is straight-line code:
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
-    auto group = [&](const int it) {
+    auto group = [&](const int it) __attribute__((always_inline)) {   // (the NCH = 4 extended kernel called it out of line: a 1.7 KB stack frame)
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
         const int g = blockIdx.x + it * p.nb;
         const int k = (g * nw + wid) * R + sub;

@@ -209,20 +209,26 @@ def test_fleet_c5_full_size_properties():
 
 
 # ------------------------------------------------------------ long horizons (H > 64)
-@pytest.mark.parametrize("H,f64", [(65, True), (100, True), (128, False), (128, True), (200, True), (256, False)])
-def test_arm_long_horizons_match_oracle(H, f64):
+@pytest.mark.parametrize("H,f64,full", [(65, True, False), (100, True, False), (128, False, False), (128, True, False),
+                                        (200, True, False), (256, False, False), (200, True, True), (256, False, True)])
+def test_arm_long_horizons_match_oracle(H, f64, full):
     """Arm at H = 65..256 (NCH = 2 and 4 DPP-scan integrator, fp32 and fp64 state; NCH = 4
     runs the 2-wave register budget; H = 65 / 100 / 200 pad the trajectory rows to 64 B)
-    against the oracle: trajectory, EE, S and the update (standard_normal_noise.py:41-48)."""
+    against the oracle: trajectory, EE, S and the update (standard_normal_noise.py:41-48).
+    ``full``: a full Sigma selects the extended (XC) kernel, whose NCH = 4 instantiation
+    once ran its rollout group out of line (a 1.7 KB stack frame)."""
     chain = _chain()
     K = 256
     torch.manual_seed(300 + H)
-    noise = O.draw_noise(K, H, torch.eye(7) * 0.1)
+    sig = np.eye(7, dtype=np.float32) * 0.1
+    if full:
+        sig[0, 1] = sig[1, 0] = 0.02
+    noise = O.draw_noise(K, H, torch.from_numpy(sig))
     u_prev = torch.randn(H, 7) * 0.3
     q_full = np.array([0.1, -0.2, 1.1, 0.0, 0.0, 0.2588190, 0.9659258] + HOME_Q)
     v_full = np.array([0.0] * 6 + [0.8, -0.5, 0.3, -1.2, 0.4, 0.9, -0.7])
     r = O.arm_step(chain, q_full, v_full, u_prev, noise, *ARM_TARGET, f64=f64)
-    e = _engine(model="arm", n_samples=K, n_horizon=H, noise="injected", state_f64=f64)
+    e = _engine(model="arm", n_samples=K, n_horizon=H, noise="injected", state_f64=f64, sigma=sig)
     e.set_target(*ARM_TARGET)
     e.set_u_prev(u_prev.numpy())
     out, u0, st = e.step(np.concatenate([q_full[:7], q_full[7:], v_full[6:]]), noise.numpy()[None])

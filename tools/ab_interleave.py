@@ -1,6 +1,6 @@
 """Interleaved same-process A/B of library builds (tools/, not shipped).
 
-    python tools/ab_interleave.py <reps> "<model K H [V nb threads]>;..." lib_a.so lib_b.so ...
+    python tools/ab_interleave.py <reps> "<model K H [V nb threads [full]]>;..." lib_a.so lib_b.so ...
 
 Every build is loaded into the one process (RTLD_LOCAL, its own kernels), an engine per
 (build, workload) is created up front, and the builds' kernel timings alternate rep by
@@ -44,8 +44,14 @@ def main():
             V = int(r[3]) if len(r) > 3 else 1
             nb = int(r[4]) if len(r) > 4 else 0
             th = int(r[5]) if len(r) > 5 else 0
+            kw = {}
+            if len(r) > 6 and r[6] == "full":   # a full Sigma: the extended (XC) kernel
+                A = {"drone": 3, "arm": 7, "wholebody": 10}[model]
+                sig = np.eye(A, dtype=np.float32) * 0.1
+                sig[0, 1] = sig[1, 0] = 0.02
+                kw["sigma"] = sig
             e = Engine(make_config(model, n_samples=K, n_horizon=H, n_vehicles=V, blocks_per_vehicle=nb,
-                                   block_threads=th, state_f64=(model == "arm")))
+                                   block_threads=th, state_f64=(model == "arm"), **kw))
             for v in range(V):
                 if model in ("drone", "quadrotor"):
                     e.set_target([1.0, 2.0, 3.4], vehicle=v)
