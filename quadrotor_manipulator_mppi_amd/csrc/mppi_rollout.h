@@ -35,6 +35,15 @@
 #ifndef MPPI_ROLL_OCC_NCH2
 #define MPPI_ROLL_OCC_NCH2 4
 #endif
+// the extended (XC) NCH == 2 kernels likewise run best at 2 (whole-body K=8192 H=128 full
+// Sigma 72.1 -> 43.6 us, arm 21.8 -> 19.3); XC NCH == 1 keeps 4 (2 and 3 measured slower;
+// profiles/r02/ab_rollout_occupancy_xc.txt)
+#ifndef MPPI_ROLL_OCC_NCH2_XC
+#define MPPI_ROLL_OCC_NCH2_XC 2
+#endif
+#ifndef MPPI_ROLL_OCC_XC
+#define MPPI_ROLL_OCC_XC 4
+#endif
 #ifndef MPPI_ROLL_OCC
 #define MPPI_ROLL_OCC 4
 #endif
@@ -590,7 +599,7 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
 // (whole-body K=8192 H=64) that is 1024 blocks x 8 waves, all resident at once: twice the
 // latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
-__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? MPPI_ROLL_OCC_NCH2 : MPPI_ROLL_OCC)) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_ctr, const uint32_t k_off,
                                                  const int32_t noise_mode, const int32_t H_arg,
                                                  const int32_t nthr,
