@@ -48,6 +48,12 @@ constexpr int kQA = 4;                     // thrust, tau_x, tau_y, tau_z
 constexpr int kQR = 16;                    // rollouts per dynamics wave (4 lanes each)
 constexpr int kQWaves = 4;                 // all draw the noise tile; wave 0 steps the dynamics
 constexpr int kQThreads = 64 * kQWaves;
+// Block size NT: 512 threads for the one-dynamics-wave variant while the grid is at most
+// 512 blocks (its phase-1 noise tile, 16 x H draws, then takes one draw per thread at
+// H <= 32 on otherwise idle SIMDs: K=4096 H=32 rollout 7.99 -> 7.83 us, H=64 12.8 -> 12.2),
+// else 256 (at 1024 blocks the extra waves only cost: K=16384 9.3 -> 9.5 us;
+// profiles/r02/ab_quadrotor_block512.txt)
+constexpr int kQThreadsWide = 512;
 
 // lane SRC of every 4-lane group, to all four (DPP quad_perm [SRC, SRC, SRC, SRC])
 template <int SRC>
@@ -72,12 +78,13 @@ __device__ __forceinline__ float qsum(float x) {
 // NWD dynamics waves per block (1 or 4): 16 rollouts per block while the grid stays at most
 // 1024 blocks (a small K spreads its noise tile and dynamics over the most CUs), 64 above
 // (fewer records for the finalize: its record loop is sequential in chunks).
-template <bool VONE, bool LIT, int NWD>
-__global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_lo, const uint32_t seed_hi,
+template <bool VONE, bool LIT, int NWD, int NT>
+__global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, const uint32_t seed_hi,
                                                             const uint32_t step_ctr, const uint32_t k_off,
                                                             const int32_t noise_mode, const int32_t H,
                                                             const float* __restrict__ u_prev, const DevParams pk) {
     static_assert(NWD == 1 || NWD == kQWaves, "dynamics waves per block");
+    static_assert(NT == kQThreads || (NWD == 1 && NT == kQThreadsWide), "block size");
     constexpr int QR = kQR * NWD;              // rollouts per block
     constexpr int kQPitch = QR * kQA + 1;      // LDS floats per t row of the eps tile (odd: the record
                                                // phase's lane = t reads are bank-conflict free)
@@ -94,7 +101,7 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
     const VehicleConst& vc = VONE ? pk.vc0 : pk.vc[v];
     if (VONE && b == 0) {   // hand vc0 to the finalize (it reads vc[v])
         constexpr int kVCW = (int)(sizeof(VehicleConst) / 4);
-        for (int i = tid; i < kVCW; i += kQThreads) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
+        for (int i = tid; i < kVCW; i += NT) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
     }
     // ---- phase 1, all waves: u_prev and the (16 x H) noise tile into LDS.  Noise
     //      (standard_normal_noise.py:22-29 / drone_mppi.py:40-44): the 4 normals of (k, t)
@@ -115,7 +122,7 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
                       "+s"(v6[0]), "+s"(v6[1]), "+s"(v6[2]), "+s"(v6[3]), "+s"(v6[4]), "+s"(v6[5]),
                       "+s"(tg3[0]), "+s"(tg3[1]), "+s"(tg3[2]), "+s"(ii3[0]), "+s"(ii3[1]), "+s"(ii3[2]),
                       "+s"(sdt), "+s"(sim), "+s"(skd), "+s"(sg), "+s"(swsp), "+s"(swtp), "+s"(scoef));
-    for (int i = tid; i < QR * H; i += kQThreads) {
+    for (int i = tid; i < QR * H; i += NT) {
         // rollouts past K replicate sample K-1 (noise and all): their lanes then compute and
         // store exactly K-1's values, so the dynamics need no store masks; weight 0 below
         const int r = i & (QR - 1), t = i / QR, k = kb + r;
@@ -306,15 +313,21 @@ __global__ void __launch_bounds__(kQThreads) k_rollout_quad(const uint32_t seed_
 }
 
 extern "C" int mppi_launch_rollout_quad(const DevParams* p, int threads, void* stream) {
-    (void)threads;   // kQThreads per block; p->iters = dynamics waves per block (1 or 4)
+    (void)threads;   // block size chosen below; p->iters = dynamics waves per block (1 or 4)
     const int nwd = p->iters;
     if (p->H > 64 || p->A != kQA || (nwd != 1 && nwd != kQWaves) || p->nb * kQR * nwd < p->K) return -1;
     const size_t lds = (size_t)((p->H + 1) * (kQR * nwd * kQA + 1) + (p->H + 1) * kQA) * sizeof(float);
     hipStream_t s = (hipStream_t)stream;
-#define MPPI_QUAD_GO(VO, LI, NW)                                                                                 \
-    hipLaunchKernelGGL((k_rollout_quad<VO, LI, NW>), dim3(p->nb, p->V), dim3(kQThreads), lds, s, p->seed_lo,    \
+    const bool wide = nwd == 1 && (size_t)p->nb * p->V <= 512;
+#define MPPI_QUAD_GO(VO, LI, NW, NT)                                                                             \
+    hipLaunchKernelGGL((k_rollout_quad<VO, LI, NW, NT>), dim3(p->nb, p->V), dim3(NT), lds, s, p->seed_lo,       \
                        p->seed_hi, p->step_ctr, (uint32_t)p->k_offset, p->noise_mode, p->H, p->u_prev, *p)
-#define MPPI_QUAD_NW(VO, LI) do { if (nwd == 1) MPPI_QUAD_GO(VO, LI, 1); else MPPI_QUAD_GO(VO, LI, kQWaves); } while (0)
+#define MPPI_QUAD_NW(VO, LI)                                                                                     \
+    do {                                                                                                         \
+        if (wide) MPPI_QUAD_GO(VO, LI, 1, kQThreadsWide);                                                        \
+        else if (nwd == 1) MPPI_QUAD_GO(VO, LI, 1, kQThreads);                                                   \
+        else MPPI_QUAD_GO(VO, LI, kQWaves, kQThreads);                                                           \
+    } while (0)
     if (p->V == 1) {
         if (p->q_literal_jinv) MPPI_QUAD_NW(true, true); else MPPI_QUAD_NW(true, false);
     } else {
