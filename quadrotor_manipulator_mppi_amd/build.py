@@ -28,11 +28,11 @@ _ASAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-po
 # v_pk_* pairings cost more register moves than they save and raise the kernel
 # from 110 to 184 VGPRs (2 instead of 4 waves per SIMD) -- DESIGN.md §kernels.
 # The kernels' leading scalar arguments (rollout: Philox key/step, sample offset,
-# noise mode, H, u_prev, joint table; finalize: record/u_prev pointers, sizes)
+# noise mode, H, u_prev, joint table; finalize: record and tail pointers, sizes, sequence)
 # are preloaded into SGPRs at wave launch.
 _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
 SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
-           ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=13"]),
+           ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=14"]),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", [])]
 HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", os.path.join("..", "..", "include", "mppi_hip.h")]
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")

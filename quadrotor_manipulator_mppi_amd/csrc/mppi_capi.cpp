@@ -316,6 +316,7 @@ struct mppi_engine {
     float* d_rdata = nullptr;   // (V,A,nb,H) block record bodies
     int fin_ts = 1, fin_tsz = 8;   // finalize t-slices
     unsigned char* d_out = nullptr;   // device scratch in h_out's layout (mppi_kernel_timing's outputs)
+    FinTail* d_tail = nullptr;        // [kTailSlots] the finalize's tail parameters per launch kind
     float* d_wraw = nullptr;
     float* d_wsmooth = nullptr;
     float* d_w = nullptr;
@@ -352,6 +353,35 @@ namespace {
 // the step goes through the exchange slots: several shards, or an engine-owned
 // communicator (a one-rank communicator runs the same pack -> all-reduce -> combine)
 bool sharded(const mppi_engine* e) { return e->cfg.shard_count > 1 || e->comm; }
+
+FinTail tail_of(const FinParams& f, int32_t mode) {
+    FinTail t;
+    std::memset(&t, 0, sizeof(t));
+    t.coef = f.coef; t.dt = f.dt; t.dt2 = f.dt2;
+    t.mode = mode; t.model = f.model; t.qoff = f.qoff; t.nq = f.nq; t.state_f64 = f.state_f64;
+    t.out_dim = f.out_dim; t.window = f.window;
+    t.u_prev = f.u_prev; t.vc = f.vc;
+    t.out = f.out; t.u0 = f.u0; t.stats = f.stats; t.flags = f.flags; t.wraw = f.wraw; t.wsmooth = f.wsmooth;
+    t.dst = f.dst; t.xbase = f.xbase; t.xslot = f.xslot; t.nslots = f.nslots; t.myslot = f.myslot; t.P = f.P;
+    std::memcpy(t.sg, f.sg, sizeof(t.sg));
+    return t;
+}
+
+// a shard's PACK fields (mppi_rollout) into FinParams, and into the PACK tail copy
+void pack_fields(const mppi_engine* e, FinParams& f) {
+    const size_t slot = (size_t)e->V * e->dp.P;
+    f.mode = 1;
+    f.dst = e->d_exchange ? e->d_exchange + slot * e->cfg.shard_rank : nullptr;
+    f.xbase = e->d_exchange; f.xslot = (int64_t)slot;
+    f.nslots = e->cfg.shard_count; f.myslot = e->cfg.shard_rank;
+}
+mppi_status upload_pack_tail(mppi_engine* e) {
+    FinParams f = e->fp;
+    pack_fields(e, f);
+    const FinTail t = tail_of(f, 1);
+    HIP_TRY(hipMemcpy(e->d_tail + kTailPack, &t, sizeof(t), hipMemcpyHostToDevice));
+    return MPPI_OK;
+}
 
 // Trajectory planes: k_rollout rows (one rollout's H steps) are padded to 64 B, hp = H
 // rounded up to 16 floats, and written whole.  With H = 100 the unpadded rows left partial
@@ -912,6 +942,28 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
     e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
     f.stamps = e->d_fstamps;
+    {   // the finalize's tail parameters, one device copy per launch kind (constant for the
+        // engine's life): the control step's FINAL, a shard's PACK, and FINAL into the device
+        // scratch outputs (mppi_kernel_timing, probes)
+        FinTail t[kTailSlots];
+        t[kTailFinal] = tail_of(f, 0);
+        t[kTailPack] = tail_of(f, 1);
+        t[kTailScratch] = tail_of(f, 0);
+        t[kTailScratch].out = (double*)e->d_out;
+        t[kTailScratch].u0 = (float*)(e->d_out + off_u0(e));
+        t[kTailScratch].stats = (float*)(e->d_out + off_stats(e));
+        t[kTailScratch].flags = (uint32_t*)(e->d_out + off_flags(e));
+        t[kTailScratch].wraw = nullptr;
+        t[kTailScratch].wsmooth = nullptr;
+        hipError_t te = hipMalloc(&e->d_tail, sizeof(t));
+        if (te == hipSuccess) te = hipMemcpy(e->d_tail, t, sizeof(t), hipMemcpyHostToDevice);
+        if (te != hipSuccess) {
+            fail(MPPI_ERR_HIP, "finalize tail parameters: %s", hipGetErrorString(te));
+            mppi_destroy(e);
+            return MPPI_ERR_HIP;
+        }
+        f.tail = e->d_tail + kTailFinal;
+    }
     *out = e;
     return MPPI_OK;
 }
@@ -937,7 +989,7 @@ void mppi_destroy(mppi_engine* e) {
     if (e->comm) rccl().destroy(e->comm);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -1018,8 +1070,9 @@ mppi_status mppi_exchange_slot_floats(mppi_engine* e, int64_t* n) {
 mppi_status mppi_bind_exchange(mppi_engine* e, float* d) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (e->comm) return fail(MPPI_ERR_STATE, "the engine owns a communicator and its exchange buffer");
+    if (use_device(e)) return MPPI_ERR_HIP;
     e->d_exchange = d;
-    return MPPI_OK;
+    return upload_pack_tail(e);
 }
 
 mppi_status mppi_comm_unique_id(uint8_t* id) {
@@ -1059,7 +1112,7 @@ mppi_status mppi_comm_init(mppi_engine* e, const uint8_t* id) {
                     r.err(rc));
     }
     e->d_exchange = e->d_xown;
-    return MPPI_OK;
+    return upload_pack_tail(e);
 }
 
 // The step's one collective: SUM all-reduce of the zero-padded slots on the engine
@@ -1118,13 +1171,10 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
     }
     if (sharded(e)) {   // fold this shard's block records into its exchange slot
-        const size_t slot = (size_t)e->V * e->dp.P;
         FinParams f = e->fp;
-        f.mode = 1;
+        pack_fields(e, f);
+        f.tail = e->d_tail + kTailPack;
         block_records(e, f);
-        f.dst = e->d_exchange + slot * e->cfg.shard_rank;
-        f.xbase = e->d_exchange; f.xslot = (int64_t)slot;
-        f.nslots = e->cfg.shard_count; f.myslot = e->cfg.shard_rank;
         rc = mppi_launch_finalize(&f, e->stream);
         if (rc != 0) return fail(MPPI_ERR_HIP, "pack launch failed (%d)", rc);
     }
@@ -1318,6 +1368,7 @@ mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us,
     f.flags = (uint32_t*)(e->d_out + off_flags(e));
     f.wraw = nullptr;
     f.wsmooth = nullptr;
+    f.tail = e->d_tail + kTailScratch;   // (the same outputs, from the kernel's device-resident copy)
     float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
     int rc = 0;
 #define KT_TRY(expr)                                                                        \
@@ -1373,6 +1424,7 @@ extern "C" mppi_status mppi_probe_sequence(mppi_engine* e, int32_t n, int32_t mo
     final_records(e, f);
     f.out = (double*)e->d_out; f.u0 = (float*)(e->d_out + off_u0(e)); f.stats = (float*)(e->d_out + off_stats(e));
     f.flags = (uint32_t*)(e->d_out + off_flags(e)); f.wraw = nullptr; f.wsmooth = nullptr;
+    f.tail = e->d_tail + kTailScratch;
     const int fb = 8 * ((e->A + 7) / 8) * ((e->H + 7) / 8) * e->V;
     hipEvent_t a, b;
     (void)hipEventCreate(&a); (void)hipEventCreate(&b);

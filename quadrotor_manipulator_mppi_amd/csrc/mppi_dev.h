@@ -119,6 +119,29 @@ struct DevParams {
 };
 constexpr int kStamps = 16;
 
+// The finalize tail's parameters, device-resident: written once at create (one copy per
+// launch kind), read by k_finalize through a preloaded pointer.  Read from the kernel
+// arguments they were cold s_loads every launch (the host writes a fresh kernel-argument
+// block per launch): ~1.1 us of the C3 finalize (profiles/r02/ab_finalize_tail_params.txt).
+struct FinTail {
+    float coef, dt, dt2;
+    int32_t mode, model, qoff, nq, state_f64, out_dim, window;
+    float* u_prev;           // (V,H,A) in/out
+    const VehicleConst* vc;  // (V)
+    double* out;
+    float* u0;
+    float* stats;
+    uint32_t* flags;
+    float* wraw;
+    float* wsmooth;
+    float* dst;              // PACK: this shard's slot, the exchange base, slot stride, count, own slot
+    float* xbase;
+    int64_t xslot;
+    int32_t nslots, myslot, P, pad_;
+    float sg[kMaxW];
+};
+enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailSlots = 3 };
+
 // Finalize / pack kernel parameters.
 struct FinParams {
     int32_t model, V, H, A, nq, qoff, state_f64;
@@ -150,6 +173,7 @@ struct FinParams {
     int32_t out_dim;
     int32_t dbg;             // diagnostic phase-skip bits (MPPI_FIN_DEBUG), 0 in production
     unsigned long long* stamps;   // diagnostic s_memtime stamps (MPPI_STAMPS), else null
+    const FinTail* tail;     // device copy of this launch kind's tail parameters
 };
 
 }  // namespace mppi

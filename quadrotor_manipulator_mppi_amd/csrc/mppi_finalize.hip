@@ -27,7 +27,7 @@ constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 wa
 constexpr int kMaxRec = 4096;
 // timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
 // outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor), 32 skips
-// the u_prev update
+// the u_prev update, 64 skips the tail parameters' kernel-argument loads
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
@@ -57,15 +57,18 @@ constexpr int kMaxRec = 4096;
 // (xor shuffles, DPP), the 8 waves through LDS behind ONE barrier, and wave 0
 // finishes alone: w_eps, SavGol by lane shuffles (WIN taps, template), u_prev,
 // outputs.
-// The leading scalar arguments (through the vehicle-constant pointer) are preloaded into
-// SGPRs (build.py: 13 dwords).
+// The leading scalar arguments (through the step's sequence number) are preloaded into
+// SGPRs (build.py: 14 dwords); the tail's parameters come from the device-resident FinTail
+// (L2-hot across steps), so a FINAL launch of one vehicle reads nothing else of its
+// kernel-argument block.  pk carries the PACK-mode fields and the diagnostic stamps.
 template <int CW, int WIN, int NT>
 __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_base,
                                                           const float* __restrict__ dat_base,
-                                                          float* __restrict__ u_prev, const uint32_t nrec_H,
-                                                          const uint32_t geo, const int32_t hdr_rs,
-                                                          const int32_t d_rs, const int32_t d_as,
-                                                          const VehicleConst* __restrict__ vcs,
+                                                          const FinTail* __restrict__ tail,
+                                                          const uint32_t nrec_H, const uint32_t geo,
+                                                          const int32_t hdr_rs, const int32_t d_rs,
+                                                          const int32_t d_as, const int32_t hdr_vs,
+                                                          const int32_t d_vs, const uint32_t seq_arg,
                                                           const FinParams pk) {
     constexpr int NWV = NT / 64;
     constexpr int ROWS = 64 / CW;          // rows per wave
@@ -87,13 +90,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3, na = (A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS;
     const int sl = j8 / na, a = x8 + MPPI_FIN_XCDS * (j8 - sl * na), v = blockIdx.y;
     if (x8 >= MPPI_FIN_XCDS || a >= A) return;
-    if (MPPI_FIN_KO & 16) { if (tid == 0) u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
+    if (MPPI_FIN_KO & 16) { if (tid == 0) p.u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
     FSTAMP(0);
     const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
     const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
-    const float* hdr = hdr_base + (v ? (size_t)v * p.hdr_vs : 0);
-    const float* col = dat_base + (v ? (size_t)v * p.d_vs : 0) + (size_t)a * d_as + w0;
-    float* up = u_prev + (size_t)v * H * A;
+    const float* hdr = hdr_base + (size_t)v * (uint32_t)hdr_vs;
+    const float* col = dat_base + (size_t)v * (uint32_t)d_vs + (size_t)a * d_as + w0;
+    const FinTail& T = *tail;
+    float* up = T.u_prev + (size_t)v * H * A;
     const int g = lane / CW, q = lane - g * CW, gr = wv * ROWS + g;
     const bool qv = q < W;
     // wave 0 prefetches u_prev over the window (lane q <-> t = w0 + q), incl. the OLD
@@ -108,33 +112,39 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // ahead of the record loads
         int vz;
         asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-        const VehicleConst* vcp = vcs + v + vz;   // vcs == p.vc, a preloaded argument
+        const VehicleConst* vcp = T.vc + v + vz;
         x0f = vcp->pos0f[a]; v0f = vcp->vel0f[a]; x0d = vcp->pos0[a]; v0d = vcp->vel0[a];
     }
 
-    // The tail's kernel arguments (FinParams fields past the preloaded ones), read into
-    // SGPRs while the record loads fly: left to the compiler, each was an s_load waited
-    // for on the spot in wave 0's tail (15 serial scalar round trips).  The empty asm
-    // makes every value opaque, so it is neither re-loaded later nor sunk to its use.
+    // The tail's parameters (FinTail), read into SGPRs while the record loads fly: left to
+    // the compiler, each was an s_load waited for on the spot in wave 0's tail (15 serial
+    // scalar round trips).  The empty asm makes every value opaque, so it is neither
+    // re-loaded later nor sunk to its use.
     float coef = 0.0f, dt = 0.0f, dt2 = 0.0f;
     int32_t mode = 0, model = 0, qoff = 0, nq = 0, sf64 = 0, odim = 0;
-    uint32_t seq = 0;
+    const uint32_t seq = seq_arg;
     float *wraw = nullptr, *wsmooth = nullptr, *u0p = nullptr, *stats = nullptr;
     double* outp = nullptr;
     uint32_t* flags = nullptr;
     float sg[WIN > 0 ? WIN : 1];
     auto pin_tail = [&]() {
-#define MPPI_PIN(x, f) do { x = f; asm volatile("" : "+s"(x)); } while (0)
-        MPPI_PIN(coef, p.coef); MPPI_PIN(dt, p.dt); MPPI_PIN(dt2, p.dt2);
-        MPPI_PIN(mode, p.mode); MPPI_PIN(model, p.model); MPPI_PIN(qoff, p.qoff); MPPI_PIN(nq, p.nq);
-        MPPI_PIN(sf64, p.state_f64); MPPI_PIN(odim, p.out_dim); MPPI_PIN(seq, p.seq);
-        MPPI_PIN(wraw, p.wraw); MPPI_PIN(wsmooth, p.wsmooth); MPPI_PIN(u0p, p.u0); MPPI_PIN(stats, p.stats);
-        MPPI_PIN(outp, p.out); MPPI_PIN(flags, p.flags);
+        // every load issues first, then two empty asms consume them (one wait): pinned one
+        // by one, each load was followed by its own s_waitcnt, ~20 serial round trips
+        coef = T.coef; dt = T.dt; dt2 = T.dt2;
+        mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
+        wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
         if constexpr (WIN > 0) {
 #pragma unroll
-            for (int j = 0; j < WIN; ++j) MPPI_PIN(sg[j], p.sg[j]);
+            for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
         }
-#undef MPPI_PIN
+        asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
+                          "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
+                          "+s"(outp), "+s"(flags));
+        if constexpr (WIN == 9)
+            asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
+                              "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
+        else if constexpr (WIN == 5)
+            asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]));
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
     // column of a row group, so each lane carries them and the wave fold runs over row groups
@@ -155,7 +165,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
             xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
         }
-        if (base == 0) pin_tail();
+        if (base == 0 && !(MPPI_FIN_KO & 64)) pin_tail();   // (64: timing knockout, tail parameters not loaded)
 #pragma unroll
         for (int i = 0; i < kNPT; ++i)
             if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
@@ -163,6 +173,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         float m = INFINITY;
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nanflag = fmaxf(nanflag, hd[i].w); }
+        // the body terms are accumulated outside the branch: used only inside it, the
+        // compiler sank the body loads into it, behind a wait for every header load (two
+        // memory round trips instead of one).  f = 0 adds exactly nothing (bodies are finite:
+        // sums of weighted noise, 0 for a block without a finite cost).
+        float fr[kNPT];
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) fr[i] = 0.0f;
         if (m < INFINITY) {
             const float rn = fminf(rho_t, m);
             if (rho_t < INFINITY) {   // rescale the running sums to the new reference
@@ -175,11 +192,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
 #pragma unroll
             for (int i = 0; i < kNPT; ++i) {
                 const float f = (hd[i].x < INFINITY) ? __expf(coef * (hd[i].x - rn)) : 0.0f;
-                acc = fmaf(f, xv[i], acc);
+                fr[i] = f;
                 eta = fmaf(f, hd[i].y, eta);
                 eta2 = fmaf(f * f, hd[i].z, eta2);
             }
         }
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) acc = fmaf(fr[i], xv[i], acc);
         FSTAMP(8);
     }
     {   // fold the wave's row groups: rescale every lane to the wave's rho, sum the rows
@@ -192,7 +211,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         if (lane == 0) { wrho[wv] = rw; wnan[wv] = nf; weta[wv] = e1; weta2[wv] = e2; }
     }
     FSTAMP(1);
-    if (MPPI_FIN_KO & 8) { if (lane < CW) u_prev[lane] += acc + (float)eta; return; }   // timing knockout
+    if (MPPI_FIN_KO & 8) { if (lane < CW) p.u_prev[lane] += acc + (float)eta; return; }   // timing knockout
     lds_barrier();
     if (wv != 0) return;
     FSTAMP(2);
@@ -213,14 +232,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int t = w0 + lane;              // this lane's time index (lanes < W)
     const bool own = lane < W && t >= t_lo && t < t_hi;
     if (mode == 1) {   // PACK raw sums into this shard's exchange slot
-        float* dst = p.dst + (size_t)v * p.P;
+        float* dst = T.dst + (size_t)v * T.P;
         if (a == 0 && sl == 0 && lane == 0) {
             dst[0] = rho; dst[1] = eta; dst[2] = eta2; dst[3] = nanf;
         }
         if (own) dst[kHdr + a * H + t] = N;
-        for (int s = 0; s < p.nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
-            if (s == p.myslot) continue;
-            float* z = p.xbase + (size_t)s * p.xslot + (size_t)v * p.P;
+        for (int s = 0; s < T.nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
+            if (s == T.myslot) continue;
+            float* z = T.xbase + (size_t)s * T.xslot + (size_t)v * T.P;
             if (a == 0 && sl == 0 && lane < kHdr) z[lane] = 0.0f;
             if (own) z[kHdr + a * H + t] = 0.0f;
         }
@@ -251,7 +270,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sm = fmaf(sg[j], src[j], sm);
         } else {
-            for (int j = 0; j < p.window; ++j) sm = fmaf(p.sg[j], src[j], sm);
+            for (int j = 0; j < T.window; ++j) sm = fmaf(T.sg[j], src[j], sm);
         }
     }
     FSTAMP(5);
@@ -320,7 +339,7 @@ __global__ void k_weights(const float* S, const float* stats, float* w, int V, i
 extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     const int W = std::min(p->H, p->tsz + 2 * p->half);
     if (p->nrec > kMaxRec || p->nrec <= 0 || p->H > MPPI_MAX_HORIZON || p->tsz > 255 || p->half > 255 ||
-        p->ts > 255 || p->A > 255 || W > 64)
+        p->ts > 255 || p->A > 255 || W > 64 || !p->tail || p->hdr_vs > 0x7fffffff || p->d_vs > 0x7fffffff)
         return -1;
     const uint32_t nh = (uint32_t)p->nrec | ((uint32_t)p->H << 16);
     const uint32_t geo = (uint32_t)p->tsz | ((uint32_t)p->half << 8) | ((uint32_t)p->ts << 16) | ((uint32_t)p->A << 24);
@@ -331,8 +350,9 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     const dim3 grid(8 * ((p->A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS) * p->ts, p->V), block(nt);   // XCD-aware map (k_finalize)
     hipStream_t s = (hipStream_t)stream;
 #define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
-    hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->u_prev, nh, geo, \
-                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, p->vc, *p)
+    hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->tail, nh, geo, \
+                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, (int32_t)p->hdr_vs,    \
+                       (int32_t)p->d_vs, p->seq, *p)
 #define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
     do {                                                                                                  \
         if (nt == 128) MPPI_FIN_GO(CWV, WINV, 128);                                                       \
