@@ -62,6 +62,11 @@ WORKLOADS = {
     # configs[4] per-GPU share: 64 vehicles x K=8192 over 8 GPUs -> 8 vehicles per GPU
     "fleet_c5": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=8,
                      desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
+    # the N=8 rank's whole step on one GPU: the C4 shard through the engine-owned RCCL
+    # communicator with one rank (rollout -> PACK -> ncclAllReduce -> finalize from C)
+    "c4_shard_native1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True,
+                             desc="Whole-body 8192 samples H=64 through a 1-rank RCCL communicator "
+                                  "(the N=8 rank's step of BASELINE configs[3])"),
 }
 
 # the CPU baseline's shapes (C4 K-reduced: the full C4 on CPU is impractical)
@@ -117,19 +122,28 @@ def set_targets(eng, model, V):
             eng.set_target(p, ARM_TARGET[1], vehicle=v)
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes of the rollout kernel from the committed rocprofv3 PMC summary
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) and where it came from."""
+def shape_key(model: str, K: int, H: int, V: int = 1) -> str:
+    """Key of one rollout launch shape in profiles/pmc_rollout.json (traffic is per shape:
+    the c4 workload's per-rank K is 65536/N)."""
+    return f"{model}_k{K}_h{H}" + (f"_v{V}" if V > 1 else "")
+
+
+def load_traffic(key: str):
+    """Per-launch HBM bytes of the rollout kernel at one launch shape (``shape_key``) from the
+    committed rocprofv3 PMC summary (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), and where
+    it came from; (None, None) for a shape without counters (never another shape's figure)."""
     path = os.path.join(ROOT, "profiles", "pmc_rollout.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
-    w = d.get(workload, {})
-    src = (f"profiles/pmc_rollout.json[{workload}]: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-           f"separate passes, avg per k_rollout launch; collected on build {w.get('build_head', '?')}")
-    return w.get("hbm_bytes_per_launch"), src if w else None
+    w = d.get(key)
+    if not w or w.get("hbm_bytes_per_launch") is None:
+        return None, None
+    src = (f"profiles/pmc_rollout.json[{key}]: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+           f"separate passes, avg per k_rollout launch of this shape; collected on build {w.get('build_head', '?')}")
+    return w["hbm_bytes_per_launch"], src
 
 
 # ------------------------------------------------------------------------------ CPU baseline
@@ -219,18 +233,45 @@ def cpu_baseline(workload: str, cell_budget_s: float):
 
 
 # ------------------------------------------------------------------------------ GPU runs
-def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
+def reduce_max(vals, dist, device):
+    """Max over ranks of a list of floats (one all-reduce on the backend's device)."""
+    if dist is None:
+        return [float(v) for v in vals]
+    import torch
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
+def timed_batches(run, n_batches, barrier):
+    """The contract's timed region, repeated: each batch is EXACTLY `steps` control steps
+    bracketed by barrier + synchronize on both sides (wall clock); returns the per-batch
+    seconds.  The line's ms_per_step is the median batch / steps (a 20-step batch is
+    ~0.2 ms, so one host hiccup at a bracket would otherwise set the number)."""
+    out = []
+    for _ in range(n_batches):
+        barrier()
+        t0 = time.perf_counter()
+        run()
+        barrier()
+        out.append(time.perf_counter() - t0)
+    return out
+
+
+def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1):
     import torch
     from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
     w = dict(WORKLOADS[name])
     w.pop("desc")
     strong = w.pop("strong", False)
+    force_native = w.pop("native", None)
     if strong:
         if w["n_samples"] % world:
             raise SystemExit(f"{name}: K={w['n_samples']} does not split over {world} ranks")
         w["n_samples"] //= world
     V = w.get("n_vehicles", 1)
-    native = None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False
+    native = force_native if force_native is not None else (
+        None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False)
     se = ShardedEngine(seed=1234, native=native, **w)
     eng = se.engine
     set_targets(eng, w["model"], V)
@@ -240,22 +281,18 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
         eng.set_u_prev(u)
     state = make_state(w["model"], V)
     eng.set_state(state)
+    red_dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else "cpu"
 
     def barrier():
+        eng.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
     se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
-    eng.synchronize()
     barrier()
-    t0 = time.perf_counter()
-    se.run_steps(steps_n)
-    eng.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
     tim = None
-    if timing:   # per-kernel HIP-event timing in its own region (events perturb the step rate)
+    if timing:   # per-kernel HIP-event timing in its own region, before the timed batches
         n_t = max(200, steps_n // 5)
         # n launches of each kernel back to back between one event pair, then n (rollout,
         # finalize) pairs as a step runs them; median of 7 batches (a transient clock dip on
@@ -267,45 +304,56 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True):
                "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
                          f"median of 7 batches, on the engine stream",
                "rollout_us_batches": [round(x, 3) for x in rs]}
-        if se.native and world > 1:   # the step's one collective alone (collective call on every rank)
+        if se.native:   # the step's one collective alone (a collective call on every rank)
             tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
-            se.run_steps(1)   # repack the slots the timing loop summed in place
-            eng.synchronize()
-    if dist is not None:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        if tim is not None:   # the slowest rank's kernels
-            r = torch.tensor([tim["rollout_us"], tim["rollout_in_step_us"]], device="cuda", dtype=torch.float64)
-            dist.all_reduce(r, op=dist.ReduceOp.MAX)
-            tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = map(float, r.tolist())
+        se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
+        barrier()
+    bt = timed_batches(lambda: se.run_steps(steps_n), batches, barrier)
+    bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
+    if tim is not None and dist is not None:   # the slowest rank's kernels
+        tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
+            [tim["rollout_us"], tim["rollout_in_step_us"]], dist, red_dev)
     # host-inclusive control-call latency (set_state H2D + step + D2H outputs + check_reach)
     lat = []
-    for i in range(lat_steps + 20):
+    for i in range(lat_steps + 20 if lat_steps else 0):
         t1 = time.perf_counter()
         se.step(state)
         if i >= 20:
             lat.append(time.perf_counter() - t1)
+    eng.synchronize()
+    if not lat:
+        se.step(state)
     out, u0, st = eng.read_outputs()
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
-    res = {"dt": dt, "tim": tim, "lat": lat, "K": eng.K, "H": eng.H, "A": eng.A, "V": V, "strong": strong,
-           "bytes": eng.rollout_bytes(), "ess": float(st[0].ess), "cfg": eng.cfg, "native": se.native,
-           "native_error": se.native_error,
-           "nranks": world}
+    comm = eng.comm_info() if se.native else None
+    res = {"batches_s": bt, "dt": float(np.median(bt)), "tim": tim, "lat": lat, "K": eng.K, "H": eng.H,
+           "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
+           "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native,
+           "native_error": se.native_error, "world": world,
+           "backend": dist.get_backend() if dist is not None else None,
+           "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None}
     eng.close()
     return res
 
 
-def roofline_of(r):
+def roofline_of(r, steps_n):
+    """Roofline of the dominant kernel (k_rollout) at this rank's launch shape, and the
+    step-level fraction: the rank's rollout bytes per control step / the step time / peak
+    (= N*bytes / step / (N*8 TB/s) for N ranks)."""
     tim = r["tim"]
     us = tim["rollout_in_step_us"]
     achieved = r["bytes"] / (us * 1e-6) / 1e9
+    step_s = r["dt"] / steps_n
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "kernel": "k_rollout_quad" if r["cfg"].model == 3 else "k_rollout",
+            "frac": achieved / HBM_PEAK_GBS, "kernel": "k_rollout_quad" if r["model"] == "quadrotor" else "k_rollout",
             "bytes_per_launch": r["bytes"], "kernel_us": us,
+            "launch_shape": shape_key(r["model"], r["K"], r["H"], r["V"]),
             "kernel_us_basis": "rollout in a control step: (rollout+finalize pair) - finalize, >= back-to-back",
-            "frac_back_to_back": r["bytes"] / (tim["rollout_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
+            "frac_back_to_back": r["bytes"] / (tim["rollout_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "frac_step": r["bytes"] / step_s / 1e9 / HBM_PEAK_GBS,
+            "frac_step_basis": "per-rank rollout bytes per control step / median step time (whole step: rollout, "
+                              "[PACK, all-reduce,] finalize) / 8 TB/s; equals N*bytes/step/(N*8 TB/s)"}
 
 
 def measured_hbm(local: int, nbytes: int = 1 << 30, reps: int = 10):
@@ -335,20 +383,101 @@ def measured_hbm(local: int, nbytes: int = 1 << 30, reps: int = 10):
     return out
 
 
+def auto_batches(steps_n: int) -> int:
+    """Timed batches for the median: 7 for short runs (the driver's --steps 20), fewer as
+    each batch gets long enough to amortise its brackets."""
+    return 7 if steps_n <= 100 else 3 if steps_n <= 1000 else 1
+
+
+def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measured=None):
+    """The one JSON line (bench contract) from rank 0's view of the max-over-ranks results."""
+    world = r["world"]
+    K, H, V = r["K"], r["H"], r["V"]
+    per_step = r["dt"] / args.steps
+    value = world * V * K * H / per_step
+    tim = r["tim"]
+    lat = np.array(r["lat"]) * 1e3
+    rf = roofline_of(r, args.steps) if tim is not None else None
+    if rf is not None:
+        traffic, traffic_src = load_traffic(rf["launch_shape"])
+        rf.update({"traffic": traffic, "traffic_source": traffic_src,
+                   "traffic_over_algorithmic": traffic / r["bytes"] if traffic else None})
+        if measured:
+            rf.update({"peak_measured": measured, "frac_of_measured_fill": rf["achieved"] / measured["fill_GBps"]})
+    w = WORKLOADS[workload]
+    line = {
+        "metric": "MPPI rollouts/sec (K x H state-steps) + control-step p50 latency, K=4096 H=32",
+        "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True,
+        "scaling": "strong" if r["strong"] else "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (reference state/goal: home joints, base at (0,0,1), mppi.py / drone_mppi.py targets; "
+                "device Philox noise)",
+        "config": {"workload": workload, "desc": w["desc"],
+                   "samples_total": world * K * V if not r["strong"] else w["n_samples"], "samples_per_gpu": K,
+                   "horizon": H, "action_dim": r["A"], "vehicles_per_gpu": V,
+                   "noise": "device Philox4x32-10 (+2x32)", "state_dtype": "f64" if r["state_f64"] else "f32",
+                   "parallelism": (f"samples sharded over {world} GPUs, 1 all-reduce/step" if world > 1
+                                   else "1 GPU")},
+        "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
+                   "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
+                   "basis": "median over the batches; each batch = exactly `steps` control steps bracketed by "
+                            "barrier + synchronize (wall clock), max over ranks"},
+        "latency_p50_ms": float(np.median(lat)) if lat.size else None,
+        "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
+        "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
+        "roofline": rf,
+        "cpu_baseline": cpu,
+        "cpu_baseline_all": cpu_all,
+        "secondary": secondary or None,
+        "build": build_info(),
+    }
+    if world > 1 or r["native"]:
+        line["multi_gpu"] = {
+            "world_size": world, "backend": r["backend"],
+            "rccl_nranks": r["rccl_nranks"], "rccl_rank": r["rccl_rank"],
+            "rccl_nranks_source": "ncclCommCount of the engine's communicator" if r["native"] else
+                                  "no RCCL communicator in this run",
+            "collective": ("engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
+                           if r["native"] else f"torch.distributed ({r['backend']}) all_reduce(SUM) of the slots"),
+            "allreduce_us": tim.get("allreduce_us") if tim else None,
+            "native_comm_error": r["native_error"],
+            "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
+            "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
+    return line
+
+
+def secondary_entry(s, ns):
+    rf = roofline_of(s, ns)
+    e = {"value": s["V"] * s["K"] * s["H"] / (s["dt"] / ns), "ms_per_step": 1e3 * s["dt"] / ns,
+         "latency_p50_ms": float(np.median(np.array(s["lat"]) * 1e3)) if s["lat"] else None,
+         "samples": s["K"], "horizon": s["H"], "vehicles": s["V"],
+         "rollout_kernel_us": rf["kernel_us"], "rollout_back_to_back_us": s["tim"]["rollout_us"],
+         "finalize_us": s["tim"]["finalize_us"], "rollout_GBps": rf["achieved"],
+         "roofline_frac": rf["frac"], "roofline_frac_back_to_back": rf["frac_back_to_back"],
+         "roofline_frac_step": rf["frac_step"]}
+    if s["native"]:
+        e.update({"allreduce_us": s["tim"].get("allreduce_us"), "rccl_nranks": s["rccl_nranks"]})
+    return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--batches", type=int, default=0, help="timed batches of --steps steps (0: auto)")
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: arm_c3 for a plain run, c4 (north star, strong scaling) under torchrun")
+    ap.add_argument("--samples", type=int, default=0,
+                    help="override the workload's samples per GPU (profiling one launch shape, e.g. the c4 "
+                         "rank shape 65536/N on one GPU)")
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--cpu-budget", type=float, default=2.5, help="seconds of CPU sampling per baseline cell")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the event-timed kernel loops (profiler runs: the trace then holds only the "
                          "control steps); no roofline in the line")
-    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4,fleet_c5,quadrotor_c2",
+    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
 
@@ -374,73 +503,28 @@ def main():
     from quadrotor_manipulator_mppi_amd import _capi
     _capi.lib()
 
+    if args.samples:
+        WORKLOADS[workload] = dict(WORKLOADS[workload], n_samples=args.samples, strong=False)
+    batches = args.batches or auto_batches(args.steps)
     r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
-                     timing=not args.no_kernel_timing)
-    K, H, V = r["K"], r["H"], r["V"]
-    per_step = r["dt"] / args.steps
-    value = world * V * K * H / per_step
-    tim = r["tim"]
-    lat = np.array(r["lat"]) * 1e3
+                     timing=not args.no_kernel_timing, batches=batches)
     secondary = {}
-    if world == 1 and args.secondary and tim is not None:
+    if world == 1 and args.secondary and r["tim"] is not None:
         for wname in [s for s in args.secondary.split(",") if s and s != workload]:
             ns = max(50, args.steps // 5)
-            s = run_workload(wname, ns, 20, 1, None, 50)
-            rf = roofline_of(s)
-            secondary[wname] = {
-                "value": s["V"] * s["K"] * s["H"] / (s["dt"] / ns), "ms_per_step": 1e3 * s["dt"] / ns,
-                "latency_p50_ms": float(np.median(np.array(s["lat"]) * 1e3)) if s["lat"] else None,
-                "samples": s["K"], "horizon": s["H"], "vehicles": s["V"],
-                "rollout_kernel_us": rf["kernel_us"], "rollout_back_to_back_us": s["tim"]["rollout_us"],
-                "finalize_us": s["tim"]["finalize_us"], "rollout_GBps": rf["achieved"],
-                "roofline_frac": rf["frac"], "roofline_frac_back_to_back": rf["frac_back_to_back"]}
+            s = run_workload(wname, ns, 20, 1, None, 50, batches=3)
+            secondary[wname] = secondary_entry(s, ns)
             log(f"secondary {wname}: {secondary[wname]}")
     cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, cpu_all = cpu_baseline(workload, args.cpu_budget)
         log(f"cpu baseline: {cpu}")
     if rank == 0:
-        traffic, traffic_src = load_traffic(workload)
-        rf = roofline_of(r) if tim is not None else None
-        if rf is not None:
-            rf.update({"traffic": traffic, "traffic_source": traffic_src})
-            if world == 1:
-                mh = measured_hbm(local)
-                rf.update({"peak_measured": mh, "frac_of_measured_fill": rf["achieved"] / mh["fill_GBps"]})
-                log(f"measured HBM: {mh}")
-        desc = WORKLOADS[workload]["desc"]
-        line = {
-            "metric": "MPPI rollouts/sec (K x H state-steps) + control-step p50 latency, K=4096 H=32",
-            "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": per_step * 1e3, "higher_is_better": True,
-            "scaling": "strong" if r["strong"] else "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (reference state/goal: home joints, base at (0,0,1), mppi.py / drone_mppi.py targets; "
-                    "device Philox noise)",
-            "config": {"workload": workload, "desc": desc, "samples_total": world * K * V if not r["strong"]
-                       else WORKLOADS[workload]["n_samples"], "samples_per_gpu": K, "horizon": H,
-                       "action_dim": r["A"], "vehicles_per_gpu": V, "noise": "device Philox4x32-10 (+2x32)",
-                       "state_dtype": "f64" if r["cfg"].state_f64 else "f32",
-                       "parallelism": (f"samples sharded over {world} GPUs, 1 all-reduce/step" if world > 1
-                                       else "1 GPU")},
-            "latency_p50_ms": float(np.median(lat)) if lat.size else None,
-            "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
-            "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
-            "roofline": rf,
-            "cpu_baseline": cpu,
-            "cpu_baseline_all": cpu_all,
-            "secondary": secondary or None,
-            "build": build_info(),
-        }
-        if world > 1:
-            line["multi_gpu"] = {
-                "rccl_nranks": r["nranks"], "collective": (
-                    "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
-                    if r["native"] else "torch.distributed all_reduce(SUM) of the slots"),
-                "allreduce_us": tim.get("allreduce_us") if tim else None,
-                "native_comm_error": r["native_error"],
-                "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
-                "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
-        print(json.dumps(line), flush=True)
+        measured = None
+        if world == 1 and r["tim"] is not None:
+            measured = measured_hbm(local)
+            log(f"measured HBM: {measured}")
+        print(json.dumps(make_line(workload, r, args, secondary, cpu, cpu_all, measured)), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

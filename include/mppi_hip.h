@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 5
+#define MPPI_ABI_VERSION 6
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
@@ -220,16 +220,27 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise);
 mppi_status mppi_finalize(mppi_engine* e);
 
 /* Native collective: one process per GPU, one engine per process.
+ * Every rank first checks mppi_comm_available (RCCL loadable, every entry point
+ * present) and the ranks agree on the outcome before any of them enters the init.
  * Rank 0 makes an id, the caller broadcasts it (torch.distributed), and every rank
- * calls mppi_comm_init with it (collective, blocking); rank/world are the config's
+ * calls mppi_comm_init with it (collective); rank/world are the config's
  * shard_rank/shard_count.  The engine then owns an RCCL communicator over xGMI and
  * its zero-padded (shard_count, V, slot) exchange buffer, and mppi_step /
  * mppi_run_steps run rollout -> pack -> ONE all-reduce(SUM) -> finalize on the engine
  * stream with no host round trip.  mppi_exchange is that all-reduce alone (split
  * phases).  A one-rank communicator runs the same sharded path on one GPU.  The
  * reference has no distributed code (mppi.py:31 pins one device). */
+mppi_status mppi_comm_available(void);
 mppi_status mppi_comm_unique_id(uint8_t id[MPPI_COMM_ID_BYTES]);
+/* The init is non-blocking with a deadline: the communicator (ncclCommInitRankConfig,
+ * blocking = 0) is polled until it is ready or timeout_ms passes (<= 0: the
+ * MPPI_COMM_INIT_TIMEOUT_MS environment value, default 60000); a communicator not
+ * ready by then is aborted and the call returns MPPI_ERR_COMM, so a rank whose peers
+ * never join returns instead of hanging.  mppi_comm_init = mppi_comm_init_ex(e, id, 0). */
 mppi_status mppi_comm_init(mppi_engine* e, const uint8_t id[MPPI_COMM_ID_BYTES]);
+mppi_status mppi_comm_init_ex(mppi_engine* e, const uint8_t id[MPPI_COMM_ID_BYTES], int32_t timeout_ms);
+/* The communicator's own rank count and rank (ncclCommCount / ncclCommUserRank). */
+mppi_status mppi_comm_info(mppi_engine* e, int32_t* nranks, int32_t* rank);
 mppi_status mppi_exchange(mppi_engine* e);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles

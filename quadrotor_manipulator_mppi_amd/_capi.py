@@ -21,7 +21,7 @@ NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 5
+ABI_VERSION = 6
 COMM_ID_BYTES = 128
 
 
@@ -96,7 +96,10 @@ PROTOTYPES = {
     "mppi_rollout": (_ST, [_P, _P]),
     "mppi_finalize": (_ST, [_P]),
     "mppi_comm_unique_id": (_ST, [C.POINTER(C.c_uint8)]),
+    "mppi_comm_available": (_ST, []),
     "mppi_comm_init": (_ST, [_P, C.POINTER(C.c_uint8)]),
+    "mppi_comm_init_ex": (_ST, [_P, C.POINTER(C.c_uint8), C.c_int32]),
+    "mppi_comm_info": (_ST, [_P, _I32, _I32]),
     "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),
     "mppi_step": (_ST, [_P, _D, _F, _D, _F, C.POINTER(Stats)]),

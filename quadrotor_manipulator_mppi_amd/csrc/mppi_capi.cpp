@@ -10,12 +10,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mppi_dev.h"
@@ -38,6 +40,13 @@ struct Rccl {
                                hipStream_t) = nullptr;
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
     const char* (*err)(ncclResult_t) = nullptr;
+    // the non-blocking init with a deadline (mppi_comm_init_ex) and the communicator's own
+    // view of its size (mppi_comm_info)
+    ncclResult_t (*init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+    ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*) = nullptr;
+    ncclResult_t (*abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*count)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*user_rank)(const ncclComm_t, int*) = nullptr;
 };
 const Rccl& rccl() {
     static const Rccl r = [] {
@@ -51,7 +60,13 @@ const Rccl& rccl() {
         x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
         x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
         x.err = (decltype(x.err))dlsym(h, "ncclGetErrorString");
-        x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.err;
+        x.init_rank_config = (decltype(x.init_rank_config))dlsym(h, "ncclCommInitRankConfig");
+        x.async_error = (decltype(x.async_error))dlsym(h, "ncclCommGetAsyncError");
+        x.abort = (decltype(x.abort))dlsym(h, "ncclCommAbort");
+        x.count = (decltype(x.count))dlsym(h, "ncclCommCount");
+        x.user_rank = (decltype(x.user_rank))dlsym(h, "ncclCommUserRank");
+        x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.err && x.init_rank_config &&
+               x.async_error && x.abort && x.count && x.user_rank;
         if (!x.ok) x.why = "librccl.so.1 lacks an nccl* entry point";
         return x;
     }();
@@ -379,6 +394,9 @@ mppi_status upload_pack_tail(mppi_engine* e) {
     FinParams f = e->fp;
     pack_fields(e, f);
     const FinTail t = tail_of(f, 1);
+    // a PACK of an earlier step may still be reading the old tail on the engine's stream
+    // (a non-blocking torch stream: the blocking copy below is not ordered against it)
+    HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemcpy(e->d_tail + kTailPack, &t, sizeof(t), hipMemcpyHostToDevice));
     return MPPI_OK;
 }
@@ -1087,32 +1105,87 @@ mppi_status mppi_comm_unique_id(uint8_t* id) {
     return MPPI_OK;
 }
 
+mppi_status mppi_comm_available(void) {
+    const Rccl& r = rccl();
+    if (!r.ok) return fail(MPPI_ERR_COMM, "RCCL unavailable: %s", r.why.c_str());
+    return MPPI_OK;
+}
+
+namespace {
+// Wait for a non-blocking communicator to leave ncclInProgress, at most until `deadline`.
+ncclResult_t comm_wait(const Rccl& r, ncclComm_t comm, std::chrono::steady_clock::time_point deadline,
+                       bool* timed_out) {
+    *timed_out = false;
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        const ncclResult_t q = r.async_error(comm, &st);
+        if (q != ncclSuccess) return q;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::steady_clock::now() >= deadline) { *timed_out = true; return ncclInProgress; }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+int init_timeout_ms() {
+    const char* s = getenv("MPPI_COMM_INIT_TIMEOUT_MS");
+    return (s && atoi(s) > 0) ? atoi(s) : 60000;
+}
+}  // namespace
+
 // Collective over all shard engines (one per process and GPU): every rank calls it
-// with the same id, rank = cfg.shard_rank, world = cfg.shard_count.  Blocks until all
-// ranks have joined.  The engine then owns the exchange buffer and runs the per-step
-// all-reduce itself (mppi_exchange; inside mppi_step / mppi_run_steps).
-mppi_status mppi_comm_init(mppi_engine* e, const uint8_t* id) {
+// with the same id, rank = cfg.shard_rank, world = cfg.shard_count.  The communicator is
+// made non-blocking (ncclCommInitRankConfig, blocking = 0) and polled until it is ready or
+// `timeout_ms` passes; then it is aborted and the call fails with MPPI_ERR_COMM, so a rank
+// whose peers never join returns instead of hanging in the init (distributed.py then
+// moves every rank to the torch.distributed collective).  The engine then owns the
+// exchange buffer and runs the per-step all-reduce itself (mppi_exchange; inside
+// mppi_step / mppi_run_steps).
+mppi_status mppi_comm_init_ex(mppi_engine* e, const uint8_t* id, int32_t timeout_ms) {
     if (!e || !id) return fail(MPPI_ERR_INVALID_ARG, "null argument");
     if (e->comm) return fail(MPPI_ERR_STATE, "communicator already initialised");
     const Rccl& r = rccl();
     if (!r.ok) return fail(MPPI_ERR_COMM, "RCCL unavailable: %s", r.why.c_str());
     if (use_device(e)) return MPPI_ERR_HIP;
+    if (timeout_ms <= 0) timeout_ms = init_timeout_ms();
     const size_t n = (size_t)e->cfg.shard_count * e->V * e->dp.P;
     HIP_TRY(hipMalloc(&e->d_xown, n * sizeof(float)));
     HIP_TRY(hipMemsetAsync(e->d_xown, 0, n * sizeof(float), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
-    const ncclResult_t rc = r.init_rank(&e->comm, e->cfg.shard_count, u, e->cfg.shard_rank);
-    if (rc != ncclSuccess) {
-        e->comm = nullptr;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    ncclComm_t comm = nullptr;
+    ncclResult_t rc = r.init_rank_config(&comm, e->cfg.shard_count, u, e->cfg.shard_rank, &cfg);
+    bool timed_out = false;
+    if ((rc == ncclSuccess || rc == ncclInProgress) && comm) rc = comm_wait(r, comm, deadline, &timed_out);
+    if (rc != ncclSuccess || !comm) {
+        if (comm) (void)r.abort(comm);   // also ends RCCL's bootstrap thread of a half-made comm
         (void)hipFree(e->d_xown);
         e->d_xown = nullptr;
-        return fail(MPPI_ERR_COMM, "ncclCommInitRank(rank %d of %d): %s", e->cfg.shard_rank, e->cfg.shard_count,
-                    r.err(rc));
+        if (timed_out)
+            return fail(MPPI_ERR_COMM, "ncclCommInitRankConfig(rank %d of %d): not ready after %d ms (aborted)",
+                        e->cfg.shard_rank, e->cfg.shard_count, (int)timeout_ms);
+        return fail(MPPI_ERR_COMM, "ncclCommInitRankConfig(rank %d of %d): %s", e->cfg.shard_rank,
+                    e->cfg.shard_count, r.err(rc));
     }
+    e->comm = comm;
     e->d_exchange = e->d_xown;
     return upload_pack_tail(e);
+}
+
+mppi_status mppi_comm_init(mppi_engine* e, const uint8_t* id) { return mppi_comm_init_ex(e, id, 0); }
+
+mppi_status mppi_comm_info(mppi_engine* e, int32_t* nranks, int32_t* rank) {
+    if (!e || !nranks || !rank) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->comm) return fail(MPPI_ERR_STATE, "mppi_comm_info needs mppi_comm_init");
+    int c = 0, u = 0;
+    ncclResult_t rc = rccl().count(e->comm, &c);
+    if (rc == ncclSuccess) rc = rccl().user_rank(e->comm, &u);
+    if (rc != ncclSuccess) return fail(MPPI_ERR_COMM, "ncclCommCount/UserRank: %s", rccl().err(rc));
+    *nranks = c;
+    *rank = u;
+    return MPPI_OK;
 }
 
 // The step's one collective: SUM all-reduce of the zero-padded slots on the engine
@@ -1122,8 +1195,15 @@ mppi_status mppi_exchange(mppi_engine* e) {
     if (!e->comm) return fail(MPPI_ERR_STATE, "mppi_exchange needs mppi_comm_init");
     if (use_device(e)) return MPPI_ERR_HIP;
     const size_t n = (size_t)e->cfg.shard_count * e->V * e->dp.P;
-    const ncclResult_t rc = rccl().all_reduce(e->d_exchange, e->d_exchange, n, ncclFloat32, ncclSum, e->comm,
-                                              e->stream);
+    ncclResult_t rc = rccl().all_reduce(e->d_exchange, e->d_exchange, n, ncclFloat32, ncclSum, e->comm,
+                                        e->stream);
+    if (rc == ncclInProgress) {   // non-blocking communicator (mppi_comm_init_ex): the enqueue
+                                  // finishes asynchronously (first call: lazy connection setup)
+        bool timed_out = false;
+        rc = comm_wait(rccl(), e->comm,
+                       std::chrono::steady_clock::now() + std::chrono::milliseconds(init_timeout_ms()), &timed_out);
+        if (timed_out) return fail(MPPI_ERR_COMM, "ncclAllReduce: not enqueued after %d ms", init_timeout_ms());
+    }
     if (rc != ncclSuccess) return fail(MPPI_ERR_COMM, "ncclAllReduce: %s", rccl().err(rc));
     return MPPI_OK;
 }

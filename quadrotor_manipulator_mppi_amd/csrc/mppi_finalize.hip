@@ -256,7 +256,9 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // LDS at kPad + (t - w0), and the lanes within hf of an edge of the horizon also write
     // their mirror position, so every owned lane reads its WIN taps at consecutive addresses
     // (immediate offsets, one wait) -- no per-tap index arithmetic, no ds_bpermute.
-    constexpr int kPad = 8;   // >= hf (window <= 17)
+    constexpr int kPad = kMaxW / 2;   // >= hf for every window create accepts (<= MPPI_MAX_SAVGOL)
+    static_assert(kPad + 64 + kMaxW / 2 <= (int)(sizeof(wsg) / sizeof(float)),
+                  "wsg holds the widest window: kPad + W (<= 64) + hf");
     float sm = 0.0f;
     if (lane < W) {
         wsg[kPad + lane] = w;

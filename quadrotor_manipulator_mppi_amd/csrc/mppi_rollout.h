@@ -134,12 +134,19 @@ __device__ __forceinline__ void philox2x10(uint32_t& c0, uint32_t& c1, uint32_t 
 __host__ __device__ __forceinline__ uint32_t philox2_key(uint32_t seed_lo, uint32_t seed_hi, uint32_t step) {
     return (seed_lo ^ (seed_hi * 0x85EBCA6Bu)) + step * 0x9E3779B9u;
 }
+// Its second counter word: (veh<<8 | t) ^ (step<<16) (t < 256 = MPPI_MAX_HORIZON).  The step
+// in the counter as well as in the key: two seeds whose folded 32-bit keys meet at some pair
+// of steps still draw different words unless the steps are equal too.  The uniform part
+// (veh<<8 ^ step<<16) is one scalar value, so the lane pays one OR, as before.
+__host__ __device__ __forceinline__ uint32_t philox2_ctr1(uint32_t veh, uint32_t t, uint32_t step) {
+    return t | ((veh << 8) ^ (step << 16));
+}
 
 // Standard normals z[a], a < NA, of sample kg at step t (noise):
 //   * normals 8j .. 8j+7 (j < NA/8): Philox4x32-10 call j, counter (kg, t, veh<<8 | j, step),
 //     key (seed lo, seed hi); word i gives the pair (8j+2i, 8j+2i+1);
 //   * the r = NA mod 8 left over: r <= 4 -> one Philox2x32-10 call, counter
-//     (kg, veh<<8 | t), key philox2_key(seed, step), its words giving pairs 8J.., 8J+2..
+//     (kg, philox2_ctr1(veh, t, step)), key philox2_key(seed, step), its words giving pairs 8J.., 8J+2..
 //     (J = NA/8); r >= 5 -> Philox4x32-10 call J as above.
 // (the whole-body's 10 dims: one 4x32 call + one 2x32 call, 30 multiplies instead of 40)
 // The draw in two halves (the rollout overlaps them with LDS latency, k_rollout): the
@@ -160,7 +167,7 @@ __device__ __forceinline__ void draw_philox(uint32_t (&w)[draw_words<NA>()], uin
         if (!(MPPI_KO & 2)) philox10(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3], s0, s1);
     }
     if constexpr (REM >= 1 && REM <= 4) {
-        w[4 * N4] = kg; w[4 * N4 + 1] = (veh << 8) | t;
+        w[4 * N4] = kg; w[4 * N4 + 1] = philox2_ctr1(veh, t, step);
         if (!(MPPI_KO & 2)) philox2x10(w[4 * N4], w[4 * N4 + 1], philox2_key(s0, s1, step));
     }
 }

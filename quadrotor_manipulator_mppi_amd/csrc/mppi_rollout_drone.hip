@@ -16,7 +16,7 @@ __device__ __forceinline__ void philox_one(uint64_t seed, uint32_t step, int veh
         raw[4 * j] = c0; raw[4 * j + 1] = c1; raw[4 * j + 2] = c2; raw[4 * j + 3] = c3;
     }
     if constexpr (REM >= 1 && REM <= 4) {
-        uint32_t c0 = kg, c1 = ((uint32_t)veh << 8) | t;
+        uint32_t c0 = kg, c1 = philox2_ctr1((uint32_t)veh, t, step);
         philox2x10(c0, c1, philox2_key((uint32_t)seed, (uint32_t)(seed >> 32), step));
         raw[4 * N4] = c0; raw[4 * N4 + 1] = c1;
     }

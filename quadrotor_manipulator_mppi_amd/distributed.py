@@ -22,8 +22,10 @@ Two ways to run the collective:
   does the all-reduce (any backend; the gloo tests on CPU and rehearsals use it).
 
 If the native communicator cannot be set up on some rank (no loadable RCCL, a bad
-unique id), every rank learns it (one MIN all-reduce of an ok flag) and all of them fall
-back to the torch.distributed collective on a fresh engine; ``native_error`` says why.
+unique id, peers that do not join before the init deadline), every rank learns it (MIN
+all-reduces of an ok flag, ``setup_native_comm``) and all of them fall back to the
+torch.distributed collective on a fresh engine; ``native_error`` says why.  RCCL's
+availability is agreed on before any rank enters the collective init.
 
 The reference has no distributed code (single process, ``CUDA_VISIBLE_DEVICES='0'``
 at ``mppi.py:31``); there is no reference collective to mirror.
@@ -77,10 +79,36 @@ def _all_ranks_ok(ok: bool, group, device: int) -> bool:
     return bool(t.item())
 
 
+def setup_native_comm(rank: int, world: int, group, device: int, available: Callable[[], Optional[str]],
+                      make_id: Callable[[], bytes], init: Callable[[bytes], None]) -> Optional[str]:
+    """Agree on, then build, the engine-owned RCCL communicator.  Returns None when every
+    rank has it, else the reason (the same verdict on every rank).
+
+    1. every rank checks that RCCL is loadable (``available``: mppi_comm_available) and the
+       ranks agree on it (MIN all-reduce) BEFORE any rank enters the collective init, so a
+       rank without RCCL cannot leave its peers waiting in ncclCommInitRankConfig;
+    2. rank 0 makes the unique id and broadcasts it (a failure is broadcast too);
+    3. every rank joins (``init``: mppi_comm_init, non-blocking with a deadline, so a rank
+       whose peers never arrive gets an error instead of hanging);
+    4. the ranks agree on the outcome (MIN all-reduce)."""
+    err = available()
+    if world > 1 and not _all_ranks_ok(err is None, group, device):
+        return err or "RCCL unavailable on another rank"
+    if err is not None:
+        return err
+    try:
+        init(share_comm_id(rank, world, group, make_id=make_id))
+    except Exception as exc:   # a bad id (every rank sees it), an init error or timeout
+        err = str(exc)
+    if world > 1 and not _all_ranks_ok(err is None, group, device):
+        return err or "another rank failed mppi_comm_init"
+    return err
+
+
 def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
     """Host restatement of the finalize combine for a (G, P) slot array -> raw
     w_eps (H, A).  Used by the CPU (gloo) tests of the exchange protocol; the
-    device path is ``k_finalize`` in mppi_kernels.hip."""
+    device path is ``k_finalize`` in csrc/mppi_finalize.hip."""
     rho = slots[:, 0].astype(np.float64)
     r = rho.min()
     f = np.exp(-(rho - r) / lam)
@@ -100,7 +128,8 @@ class ShardedEngine:
         if native is None:
             native = self.world > 1 and dist.get_backend(group) == "nccl" and exchange is all_reduce_slots
         self.native = bool(native)
-        self.local = int(os.environ.get("LOCAL_RANK", engine_kw.pop("device", 0)))
+        device = engine_kw.pop("device", 0)
+        self.local = int(os.environ.get("LOCAL_RANK", device))
         self.local %= max(1, torch.cuda.device_count())   # more ranks than devices: wrap
         torch.cuda.set_device(self.local)
         cfg = make_config(device=self.local, shard_rank=self.rank, shard_count=self.world, **engine_kw)
@@ -113,16 +142,13 @@ class ShardedEngine:
         self.buf: Optional[torch.Tensor] = None
         self.native_error: Optional[str] = None
         if self.native:   # engine-owned RCCL communicator: the whole step is enqueued from C
-            err = None
-            try:
-                self.engine.comm_init(share_comm_id(self.rank, self.world, group))
-            except Exception as exc:   # e.g. no loadable RCCL (every rank sees it: checked below)
-                err = str(exc)
-            if self.world > 1 and not _all_ranks_ok(err is None, group, self.local):
+            err = setup_native_comm(self.rank, self.world, group, self.local, Engine.comm_available,
+                                    Engine.comm_unique_id, self.engine.comm_init)
+            if err is not None and self.world > 1:
                 # a failure on any rank: every rank takes the torch.distributed collective
                 # instead (same slots, same finalize) on a fresh engine, so no rank is left
                 # waiting in a collective alone
-                self.native_error = err or "another rank failed mppi_comm_init"
+                self.native_error = err
                 self.native = False
                 self.engine.close()
                 self.engine = Engine(cfg)

@@ -186,12 +186,28 @@ class Engine:
         capi.check(capi.lib().mppi_comm_unique_id(buf), "comm_unique_id")
         return bytes(buf)
 
-    def comm_init(self, uid: bytes):
-        """Join the shard communicator (collective over cfg.shard_count ranks)."""
+    @staticmethod
+    def comm_available() -> Optional[str]:
+        """None if RCCL is loadable with every entry point the engine binds, else why not."""
+        L = capi.lib()
+        if L.mppi_comm_available() == capi.OK:
+            return None
+        return L.mppi_last_error().decode(errors="replace")
+
+    def comm_init(self, uid: bytes, timeout_ms: int = 0):
+        """Join the shard communicator (collective over cfg.shard_count ranks).  Non-blocking
+        init polled until ``timeout_ms`` (0: MPPI_COMM_INIT_TIMEOUT_MS, default 60 s); raises
+        MPPIError(ERR_COMM) when the peers do not join in time."""
         if len(uid) != capi.COMM_ID_BYTES:
             raise ValueError("comm id must be %d bytes" % capi.COMM_ID_BYTES)
         buf = (C.c_uint8 * capi.COMM_ID_BYTES).from_buffer_copy(uid)
-        capi.check(self._L.mppi_comm_init(self._h, buf), "comm_init")
+        capi.check(self._L.mppi_comm_init_ex(self._h, buf, int(timeout_ms)), "comm_init")
+
+    def comm_info(self):
+        """(nranks, rank) as the RCCL communicator itself reports them."""
+        n, r = C.c_int32(), C.c_int32()
+        capi.check(self._L.mppi_comm_info(self._h, C.byref(n), C.byref(r)), "comm_info")
+        return n.value, r.value
 
     def exchange(self):
         capi.check(self._L.mppi_exchange(self._h), "exchange")

@@ -1,6 +1,6 @@
 """HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-    python scripts/pmc_traffic.py <pmc dir> <workload> [--merge profiles/pmc_rollout.json]
+    python scripts/pmc_traffic.py <pmc dir> <shape key> [--merge profiles/pmc_rollout.json] [--workload spec]
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM), so
@@ -51,8 +51,9 @@ def main():
                                                "quadrotor_manipulator_mppi_amd", "lib", "BUILD_INFO.json")))["git_head"]
         except (OSError, ValueError, KeyError):
             head = "?"
+        spec = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else workload
         allw[workload] = {"hbm_bytes_per_launch": roll.get("hbm_bytes_per_launch"), "kernels": rec,
-                          "build_head": head, "collected": root,
+                          "build_head": head, "collected": root, "workload": spec,
                           "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes, avg per dispatch"}
         json.dump(allw, open(out, "w"), indent=1)
 

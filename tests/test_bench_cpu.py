@@ -1,0 +1,107 @@
+"""bench.py's JSON line without a GPU: the fields the driver's multi-GPU scaling run reads
+are built from the measurements the way a torchrun launch builds them.  Two gloo ranks
+stand in for two GPUs: each reports its own batch times and kernel times, ``reduce_max``
+takes the max over ranks, and rank 0 builds the line with ``make_line``."""
+import argparse
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _fake_result(world, rank, model="wholebody", K=8192, H=64, native=False, backend="gloo"):
+    rng = np.random.default_rng(rank)
+    return {"batches_s": list(20 * 20e-6 * (1 + 0.05 * rng.random(7)) * (1 + rank)), "dt": None,
+            "tim": {"rollout_us": 12.5 + rank, "finalize_us": 4.8, "pair_us": 17.4 + rank,
+                    "rollout_in_step_us": 12.6 + rank, "method": "fake"},
+            "lat": [3e-5] * 10, "K": K, "H": H, "A": 10, "V": 1, "strong": True,
+            "bytes": K * H * 88 + 4 * K, "ess": 1.0, "model": model, "state_f64": False, "native": native,
+            "native_error": None, "world": world, "backend": backend,
+            "rccl_nranks": world if native else None, "rccl_rank": rank if native else None}
+
+
+def _args(steps=20):
+    return argparse.Namespace(steps=steps, warmup=5)
+
+
+def _rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r = _fake_result(world, rank, K=65536 // world)
+        r["batches_s"] = bench.reduce_max(r["batches_s"], dist, "cpu")
+        r["dt"] = float(np.median(r["batches_s"]))
+        t = r["tim"]
+        t["rollout_us_max_over_ranks"], t["rollout_in_step_us_max_over_ranks"] = bench.reduce_max(
+            [t["rollout_us"], t["rollout_in_step_us"]], dist, "cpu")
+        q.put((rank, bench.make_line("c4", r, _args()) if rank == 0 else None, r["batches_s"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_line_two_gloo_ranks():
+    """The SCALE line of a 2-rank gloo rehearsal: no RCCL communicator is claimed
+    (rccl_nranks null, backend gloo), the batch times are the max over ranks, the roofline
+    is the rank's own launch shape (K = 65536/2) with traffic of that shape only, and the
+    step-level fraction is N*bytes/step/(N*8 TB/s)."""
+    world = 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    line = res[0][1]
+    assert res[0][2] == res[1][2], "every rank holds the max-over-ranks batch times"
+    worst = [max(a, b) for a, b in zip(_fake_result(2, 0)["batches_s"], _fake_result(2, 1)["batches_s"])]
+    assert np.allclose(res[0][2], worst)
+    mg = line["multi_gpu"]
+    assert mg["rccl_nranks"] is None and mg["backend"] == "gloo" and mg["world_size"] == 2
+    assert "gloo" in mg["collective"]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["samples_per_gpu"] == 32768 and line["config"]["samples_total"] == 65536
+    step = float(np.median(worst)) / 20
+    assert line["ms_per_step"] == pytest.approx(step * 1e3)
+    assert line["value"] == pytest.approx(2 * 32768 * 64 / step)
+    assert line["timing"]["timed_batches"] == 7
+    rf = line["roofline"]
+    assert rf["launch_shape"] == "wholebody_k32768_h64"
+    assert rf["bytes_per_launch"] == 32768 * 64 * 88 + 4 * 32768
+    bytes_ = rf["bytes_per_launch"]
+    assert rf["frac_step"] == pytest.approx(2 * bytes_ / step / (2 * 8e12))
+    if rf["traffic"] is not None:   # counters of exactly this shape, never another shape's
+        assert 1.0 <= rf["traffic_over_algorithmic"] < 1.1
+        assert "wholebody_k32768_h64" in rf["traffic_source"]
+    assert line["kernels"]["rollout_in_step_us_max_over_ranks"] == pytest.approx(13.6)
+
+
+def test_bench_line_native_one_rank_and_traffic_by_shape():
+    """A 1-rank RCCL run names the communicator's own rank count; traffic is looked up by
+    launch shape (the N=8 c4 rank shape has counters; a shape without any gets null)."""
+    r = _fake_result(1, 0, native=True, backend=None)
+    r["dt"] = float(np.median(r["batches_s"]))
+    line = bench.make_line("c4_shard_native1", r, _args())
+    assert line["multi_gpu"]["rccl_nranks"] == 1
+    assert "ncclCommCount" in line["multi_gpu"]["rccl_nranks_source"]
+    rf = line["roofline"]
+    assert rf["launch_shape"] == "wholebody_k8192_h64"
+    assert rf["traffic"] is not None and 1.0 <= rf["traffic_over_algorithmic"] < 1.1
+    r = _fake_result(1, 0, K=1000)
+    r["dt"] = float(np.median(r["batches_s"]))
+    assert bench.make_line("wholebody_c4", r, _args())["roofline"]["traffic"] is None
+    assert bench.load_traffic("wholebody_k1000_h64") == (None, None)
+
+
+def test_auto_batches():
+    assert bench.auto_batches(20) == 7 and bench.auto_batches(500) == 3 and bench.auto_batches(5000) == 1

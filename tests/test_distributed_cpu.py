@@ -19,7 +19,8 @@ import torch.multiprocessing as mp
 
 from conftest import load_golden
 from oracle import mppi_oracle as O
-from quadrotor_manipulator_mppi_amd.distributed import HDR, all_reduce_slots, combine_slots, share_comm_id
+from quadrotor_manipulator_mppi_amd.distributed import (HDR, all_reduce_slots, combine_slots, setup_native_comm,
+                                                        share_comm_id)
 
 
 def _slot_len(A, H):
@@ -182,9 +183,62 @@ def test_native_comm_entry_points_reject_bad_arguments():
     assert L.mppi_comm_unique_id(None) == capi.ERR_INVALID_ARG
     buf = (C.c_uint8 * capi.COMM_ID_BYTES)()
     assert L.mppi_comm_init(None, buf) == capi.ERR_INVALID_ARG
+    assert L.mppi_comm_init_ex(None, buf, 100) == capi.ERR_INVALID_ARG
+    n, r_ = C.c_int32(), C.c_int32()
+    assert L.mppi_comm_info(None, C.byref(n), C.byref(r_)) == capi.ERR_INVALID_ARG
     assert L.mppi_exchange(None) == capi.ERR_INVALID_ARG
     us = C.c_double()
     assert L.mppi_exchange_timing(None, 10, C.byref(us)) == capi.ERR_INVALID_ARG
     r, f, pr = C.c_double(), C.c_double(), C.c_double()
     assert L.mppi_kernel_timing_ex(None, 10, C.byref(r), C.byref(f), C.byref(pr)) == capi.ERR_INVALID_ARG
     assert "bad arguments" in L.mppi_last_error().decode()
+
+
+def _setup_rank(rank, world, port, q, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def available():
+            return "RCCL unavailable: librccl.so.1: cannot open" if (fault == "unavailable" and rank == 1) else None
+
+        def init(uid):
+            calls.append(len(uid))
+            if fault == "timeout" and rank == 1:   # what mppi_comm_init_ex raises at its deadline
+                raise RuntimeError("[mppi status -5] comm_init: ncclCommInitRankConfig(rank 1 of 2): "
+                                   "not ready after 100 ms (aborted)")
+        err = setup_native_comm(rank, world, None, 0, available, lambda: bytes(range(128)), init)
+        q.put((rank, err, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault", [None, "unavailable", "timeout"])
+def test_native_comm_setup_agreement_world2(fault):
+    """distributed.setup_native_comm under gloo: the ranks agree on RCCL's availability
+    before any of them enters the collective init (a rank without RCCL must not leave rank 0
+    waiting in ncclCommInitRankConfig), and an init that times out on one rank (the
+    non-blocking init's deadline) gives every rank the same failure -- the cue for all of
+    them to take the torch.distributed collective -- instead of a stuck rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_setup_rank, args=(r, world, port, q, fault)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if fault is None:
+        assert [r[1] for r in res] == [None, None]
+        assert [r[2] for r in res] == [[128], [128]]
+    elif fault == "unavailable":
+        assert all(r[1] and "RCCL unavailable" in r[1] for r in res)
+        assert [r[2] for r in res] == [[], []], "no rank may enter the init"
+    else:
+        assert all(r[1] for r in res)
+        assert "not ready after" in res[1][1]
+        assert [r[2] for r in res] == [[128], [128]]

@@ -287,10 +287,13 @@ def test_output_sequence_survives_step_counter_rewind():
 # ------------------------------------------ SavGol windows (finalize template / generic path)
 @pytest.mark.parametrize("model,H,window,order", [("arm", 32, 7, 3), ("arm", 16, 11, 2), ("arm", 32, 3, 1),
                                                   ("drone", 20, 9, 2), ("drone", 64, 13, 4),
-                                                  ("wholebody", 64, 5, 2)])
+                                                  ("wholebody", 64, 5, 2), ("arm", 32, 19, 2),
+                                                  ("arm", 32, 31, 2), ("drone", 20, 19, 3),
+                                                  ("wholebody", 64, 31, 4)])
 def test_savgol_windows_match_oracle(model, H, window, order):
     """The finalize's SavGol for every window class: the templated 9- and 5-tap kernels
-    and the generic one (3, 7, 11, 13 taps), at horizons whose slices put the reflected
+    and the generic one (3, 7, 11, 13, 19, 31 taps: half-widths up to MPPI_MAX_SAVGOL/2 = 15,
+    the LDS pad's full depth), at horizons whose slices put the reflected
     pads (svg_filter.py:58) inside the window; checked as the reference filter of the
     device's own raw weighted noise (rtol 1e-5), and the update u += SavGol(w_eps)."""
     A = {"arm": 7, "drone": 3, "wholebody": 10}[model]
@@ -318,3 +321,79 @@ def test_savgol_windows_match_oracle(model, H, window, order):
     scale = float(np.abs(raw[0]).max())
     _close(sm[0], want, rtol=1e-5, atol=1e-6 * scale, what=f"{model} H={H} savgol({window},{order})")
     _close(up, u_prev + sm[0], rtol=1e-6, atol=1e-7, what="u_prev += w_eps")
+
+
+# ----------------------------------------- extended (XC) kernel: drone full Sigma, generic chain
+def test_drone_full_sigma_extended_kernel():
+    """A non-diagonal Sigma sends the drone rollout to the extended (XC) instantiation
+    (it used to stay on the common kernel): trajectory, S, the reduction, u_prev and the
+    outputs against O.drone_step (drone_mppi.py:140-176) on the same injected noise; and in
+    device-noise mode the stored eps equals z Sigma (row vector, drone_mppi.py:41-43) of the
+    Philox normals."""
+    K, H = 512, 32
+    sig = np.diag([30.0, 30.0, 30.0]).astype(np.float32)
+    sig[0, 1] = sig[1, 0] = 6.0
+    sig[1, 2] = sig[2, 1] = -4.0
+    torch.manual_seed(71)
+    noise = O.draw_noise(K, H, torch.from_numpy(sig))
+    u_prev = torch.randn(H, 3) * 2.0
+    x, v, tgt = [0.0, 0.0, 1.0], [0.1, -0.1, 0.0], [1.0, 2.0, 3.4]
+    ref = O.drone_step(x, v, u_prev, noise, tgt)
+    e = _engine(model="drone", n_samples=K, n_horizon=H, noise="injected", sigma=sig)
+    e.set_target(np.asarray(tgt, np.float32))
+    e.set_u_prev(u_prev.numpy())
+    out, u0, st = e.step(np.array(x + v, np.float64), noise.numpy()[None])
+    _close(e.get_trajectory()[0], ref["traj"].numpy(), atol=2e-5, what="drone traj (full Sigma)")
+    S = e.get_costs()[0]
+    _close(S, ref["S"].numpy(), rtol=2e-5, what="drone S (full Sigma)")
+    raw, sm = e.get_weighted_noise()
+    u0_tol = _check_reduction(S, raw[0], sm[0], e.get_u_prev()[0], ref, noise.numpy(), 5, "drone full Sigma")
+    _close(out[0, :3], ref["x_out"].numpy(), atol=max(1e-6, u0_tol * 1e-4), what="x")
+    _close(out[0, 3:], ref["v_out"].numpy(), atol=max(1e-5, u0_tol * 1e-2), what="v")
+    e.close()
+    from quadrotor_manipulator_mppi_amd.engine import philox_normals
+    e = _engine(model="drone", n_samples=K, n_horizon=H, sigma=sig, seed=3, store_noise=True)
+    e.set_target(np.asarray(tgt, np.float32))
+    e.step(np.array(x + v, np.float64))
+    eps = e.get_noise()[0]
+    e.close()
+    _, z = philox_normals(3, 0, 0, 0, K, H, 3)
+    _close(eps, z @ sig, rtol=1e-5, atol=1e-4, what="eps = z Sigma (device noise, full Sigma)")
+
+
+@pytest.mark.parametrize("kinova_path_off", [False, True])
+def test_arm_generic_chain_extended_kernel(kinova_path_off, monkeypatch):
+    """Arm chains other than the Kinova axis-permutation chain run the generic FK (one 3x4
+    affine product and one sincos per joint) in the extended (XC) instantiation: a URDF
+    whose joint origins are not signed axis permutations (joint 3 tilted, joint 5 offset),
+    and the shipped chain with the Kinova path disabled (MPPI_NO_KINOVA_PATH) -- each against
+    the oracle's chain product (urdfparser.py:122-163) on the same injected noise."""
+    from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain
+    chain_d = [dict(j) for j in load_chain()]
+    if kinova_path_off:
+        monkeypatch.setenv("MPPI_NO_KINOVA_PATH", "1")
+    else:
+        chain_d[3]["rpy"] = [float(chain_d[3]["rpy"][0]) + 0.13, float(chain_d[3]["rpy"][1]) - 0.07,
+                             float(chain_d[3]["rpy"][2])]
+        chain_d[5]["xyz"] = [float(chain_d[5]["xyz"][0]) + 0.011, float(chain_d[5]["xyz"][1]),
+                             float(chain_d[5]["xyz"][2]) - 0.02]
+    chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in chain_d]
+    K, H = 512, 32
+    torch.manual_seed(91)
+    noise = O.draw_noise(K, H, torch.eye(7) * 0.1)
+    u_prev = torch.randn(H, 7) * 0.3
+    q_full = np.array([0.1, -0.2, 1.1, 0.0, 0.0, 0.2588190, 0.9659258] + HOME_Q)
+    v_full = np.array([0.0] * 6 + [0.8, -0.5, 0.3, -1.2, 0.4, 0.9, -0.7])
+    r = O.arm_step(chain, q_full, v_full, u_prev, noise, *ARM_TARGET, f64=True)
+    e = _engine(model="arm", n_samples=K, n_horizon=H, noise="injected", chain=chain_d)
+    e.set_target(*ARM_TARGET)
+    e.set_u_prev(u_prev.numpy())
+    e.step(np.concatenate([q_full[:7], q_full[7:], v_full[6:]]), noise.numpy()[None])
+    tr = e.get_trajectory()[0]
+    _close(tr[..., :7], r["q_samples"].numpy(), atol=2e-6, what="q")
+    _close(tr[..., 7:], r["ee"].numpy().reshape(K, H, 16), atol=2e-5, what="EE (generic chain)")
+    S = e.get_costs()[0]
+    _close(S, r["S"].numpy(), rtol=2e-5, what="S (generic chain)")
+    raw, sm = e.get_weighted_noise()
+    _check_reduction(S, raw[0], sm[0], e.get_u_prev()[0], r, noise.numpy(), 9, "arm generic chain")
+    e.close()

@@ -197,6 +197,14 @@ def test_philox_streams_are_distinct():
     assert raw0.shape == (64, 32, 6)
     for other in (raw1, raw2):
         assert not np.any(raw0[..., 4] == other[..., 4]) or np.mean(raw0[..., 4] == other[..., 4]) < 1e-3
+    # two seeds whose folded 32-bit keys meet at different steps: the step in the counter
+    # (philox2_ctr1) still separates their remainder words
+    sa = 0x1234567
+    sb = (sa - 0x9E3779B9) & 0xFFFFFFFF
+    assert O.philox2_key(sa, 0) == O.philox2_key(sb, 1)
+    ra, _ = O.philox_normals(sa, 0, 0, np.arange(64), 32, 3)
+    rb, _ = O.philox_normals(sb, 1, 0, np.arange(64), 32, 3)
+    assert np.mean(ra == rb) < 1e-3
 
 
 def test_philox_normals_moments():
