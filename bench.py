@@ -480,6 +480,12 @@ def main():
     ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
+    # the JSON line is the only thing on stdout: keep the real stdout for it and send fd 1 to
+    # stderr, so native libraries that print there (RCCL's version banner at communicator
+    # init) cannot add lines to it
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     import torch
     launched = "WORLD_SIZE" in os.environ
@@ -524,7 +530,7 @@ def main():
         if world == 1 and r["tim"] is not None:
             measured = measured_hbm(local)
             log(f"measured HBM: {measured}")
-        print(json.dumps(make_line(workload, r, args, secondary, cpu, cpu_all, measured)), flush=True)
+        print(json.dumps(make_line(workload, r, args, secondary, cpu, cpu_all, measured)), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

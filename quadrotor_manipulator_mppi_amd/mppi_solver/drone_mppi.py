@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from ..engine import Engine, make_config
+from ._outputs import OutputRing
 
 
 class MPPI:
@@ -43,6 +44,7 @@ class MPPI:
         self._lock = threading.Lock()
         self._engine: Optional[Engine] = None
         self._u_prev_host = np.zeros((n_timestep, 3), np.float32)
+        self._out_ring = OutputRing(self.device, 6)   # (x, v): one async H2D copy per call
 
     def _ensure_engine(self, noise: str) -> Engine:
         e = self._engine
@@ -88,9 +90,8 @@ class MPPI:
         self.last_stats = stats[0]
         if self.verbose:
             print("Rho :", torch.tensor(stats[0].rho))
-        xo = torch.tensor(out[0, :3], dtype=torch.float32, device=self.device)
-        vo = torch.tensor(out[0, 3:6], dtype=torch.float32, device=self.device)
-        return xo, vo
+        t = self._out_ring.to_device(out[0, :6])
+        return t[:3], t[3:6]
 
     def compute_weights(self, S: torch.Tensor) -> torch.Tensor:
         rho = S.min()

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from ..engine import Engine, make_config
+from ._outputs import OutputRing
 
 
 class MPPI:
@@ -27,6 +28,7 @@ class MPPI:
                  noise: str = "philox", seed: int = 0x5EED, mass: float = 14.7,
                  inertia=(1.57, 3.93, 2.59), kd: float = 0.0, gravity: float = 9.81, verbose: bool = False):
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
+        self._out_ring = OutputRing(self.device, 12)   # (x_des, v_des): one async H2D copy per call
         self._dev_index = device or 0
         self.n_samples = n_samples
         self.n_timestep = n_timestep
@@ -90,8 +92,8 @@ class MPPI:
         self.last_stats = stats[0]
         if self.verbose:
             print("Rho :", torch.tensor(stats[0].rho))
-        xo = torch.tensor(out[0, :6], dtype=torch.float32, device=self.device)
-        vo = torch.tensor(out[0, 6:12], dtype=torch.float32, device=self.device)
+        t = self._out_ring.to_device(out[0, :12])   # one async H2D copy per call
+        xo, vo = t[:6], t[6:12]
         return xo, vo
 
     def compute_weights(self, S: torch.Tensor) -> torch.Tensor:

@@ -31,6 +31,8 @@ Fixture map:
                               path end to end at the plain 1e-4 rel bar, 2 steps
 
 Regenerate one fixture only:  python tests/golden/make_golden.py --only arm_k32_h32_gap
+Write into another directory: python tests/golden/make_golden.py --out DIR
+(tests/test_golden_regen.py does that and compares every array with the committed ones.)
 """
 import contextlib
 import io
@@ -395,7 +397,8 @@ def make_wholebody(path, K, H, steps, seed0):
 
 def main():
     torch.set_num_threads(1)
-    d = HERE
+    d = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else HERE
+    os.makedirs(d, exist_ok=True)
     if "--only" in sys.argv:
         only = sys.argv[sys.argv.index("--only") + 1]
         FIXTURES[only](d)

@@ -319,7 +319,17 @@ def test_savgol_windows_match_oracle(model, H, window, order):
     e.close()
     want = O.savgol(torch.from_numpy(raw[0].astype(np.float32)), window, order).numpy()
     scale = float(np.abs(raw[0]).max())
-    _close(sm[0], want, rtol=1e-5, atol=1e-6 * scale, what=f"{model} H={H} savgol({window},{order})")
+    # the engine's taps are the fp64 least-squares solution rounded to fp32; the reference
+    # inverts A^T A in fp32 (svg_filter.py:52-55), which for a wide window of high order is
+    # ill-conditioned (31 taps, order 4: its taps are 9e-6 off the exact ones, 1e-7 at the
+    # reference's own 5/2 and 9/2).  The bar adds that tap error times the signal.
+    half = window // 2
+    x = np.arange(-half, half + 1, dtype=np.float64)
+    Av = np.vander(x, order + 1, increasing=True)
+    exact = (np.linalg.inv(Av.T @ Av) @ Av.T)[0]
+    tap_err = float(np.abs(O.savgol_coefficients(window, order).numpy() - exact).sum())
+    _close(sm[0], want, rtol=1e-5, atol=1e-6 * scale + 2.0 * tap_err * scale,
+           what=f"{model} H={H} savgol({window},{order})")
     _close(up, u_prev + sm[0], rtol=1e-6, atol=1e-7, what="u_prev += w_eps")
 
 

@@ -414,6 +414,7 @@ def test_dropin_drone_class_reference_call_pattern():
     from quadrotor_manipulator_mppi_amd.mppi_solver.drone_mppi import MPPI
     g = load_golden("drone_k128_h20.npz")
     m = MPPI(n_samples=128, n_timestep=20)
+    held = []
     for s in range(3):
         m.u_prev = torch.from_numpy(g[f"s{s}_u_prev_in"])
         m.set_state(g[f"s{s}_x_in"].tolist(), g[f"s{s}_v_in"].tolist())
@@ -422,6 +423,12 @@ def test_dropin_drone_class_reference_call_pattern():
         _close(x.cpu().numpy(), g[f"s{s}_x_out"], atol=1e-6, what="x")
         _close(v.cpu().numpy(), g[f"s{s}_v_out"], atol=1e-5, what="v")
         assert isinstance(x.to("cpu").tolist(), list)   # drone.py:240
+        held.append((x, v))
+    for _ in range(20):   # more calls than the staging ring is deep (one async H2D copy per call)
+        m.compute_control_input()
+    for s, (x, v) in enumerate(held):   # a returned tensor is the caller's: never overwritten later
+        _close(x.cpu().numpy(), g[f"s{s}_x_out"], atol=1e-6, what="held x")
+        _close(v.cpu().numpy(), g[f"s{s}_v_out"], atol=1e-5, what="held v")
 
 
 # ------------------------------------------------------- multi-rank (gloo, 1 GPU)
