@@ -20,9 +20,31 @@ def golden_dir():
     return GOLDEN
 
 
-def load_golden(name):
+REFERENCE = os.environ.get("MPPI_REFERENCE_ROOT", "/root/reference")
+
+
+def load_golden_from(root, name):
     import numpy as np
-    return dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
+    return dict(np.load(os.path.join(root, name), allow_pickle=False))
+
+
+def load_golden(name):
+    return load_golden_from(GOLDEN, name)
+
+
+@pytest.fixture(scope="session")
+def fresh_golden_dir(tmp_path_factory):
+    """Fixtures regenerated from the reference on this host (``make_golden.py``, ~2 s),
+    or None where /root/reference is absent (the GPU box)."""
+    import subprocess
+    if not os.path.isdir(os.path.join(REFERENCE, "src", "mav_mppi")):
+        return None
+    out = tmp_path_factory.mktemp("golden_fresh")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, os.path.join(GOLDEN, "make_golden.py"), "--out", str(out)],
+                       cwd=str(out), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return str(out)
 
 
 @pytest.fixture(scope="session")

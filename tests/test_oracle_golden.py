@@ -1,14 +1,27 @@
 """Pin the CPU oracle against the golden fixtures generated from the reference.
 
-The oracle restates the reference's torch-CPU op sequence, so these checks are
-BIT-EXACT (``torch.equal``) unless a comment says otherwise.  CPU only.
+Every test runs twice:
+
+* ``fresh`` -- against fixtures ``tests/golden/make_golden.py`` regenerates from
+  /root/reference on THIS host (skipped where the reference is absent).  The
+  oracle restates the reference's torch-CPU op sequence, so these checks are
+  BIT-EXACT (``torch.equal``): same host, same libm/SIMD dispatch, same bits.
+* ``committed`` -- against the committed fixtures.  They were made on another
+  host; torch's vectorised transcendentals and reductions differ across CPU
+  microarchitectures by an ulp or so (measured: norm-wise <= 6e-7, see
+  DESIGN.md §5), so these checks hold the oracle to CROSS_HOST_RTOL of each
+  array's largest magnitude.  Bit-exact where the host is the one that made them.
+
+Unless a comment says otherwise.  CPU only.
 """
 import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
+from conftest import GOLDEN, load_golden_from
 from oracle import mppi_oracle as O
+
+CROSS_HOST_RTOL = 4e-6
 
 
 def _eq(a, b):
@@ -16,6 +29,40 @@ def _eq(a, b):
     b = torch.as_tensor(np.asarray(b))
     assert a.dtype == b.dtype, (a.dtype, b.dtype)
     assert torch.equal(a, b), f"max|d|={(a.double() - b.double()).abs().max().item()}"
+
+
+def _close_cross_host(a, b):
+    a = torch.as_tensor(np.asarray(a))
+    b = torch.as_tensor(np.asarray(b))
+    assert a.dtype == b.dtype, (a.dtype, b.dtype)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if torch.equal(a, b) or not a.is_floating_point():
+        assert torch.equal(a, b)
+        return
+    d = (a.double() - b.double()).abs().max().item()
+    scale = b.double().abs().max().item()
+    assert d <= CROSS_HOST_RTOL * scale, f"max|d|={d} scale={scale}"
+
+
+class _Golden:
+    def __init__(self, root, exact):
+        self.root, self.exact = root, exact
+
+    def load(self, name):
+        return load_golden_from(self.root, name)
+
+    def eq(self, a, b):
+        (_eq if self.exact else _close_cross_host)(a, b)
+
+
+@pytest.fixture(params=["committed", "fresh"])
+def golden(request):
+    if request.param == "committed":
+        return _Golden(GOLDEN, exact=False)
+    fresh = request.getfixturevalue("fresh_golden_dir")
+    if fresh is None:
+        pytest.skip("reference not present: no same-host fixtures to hold the oracle bit-exact to")
+    return _Golden(fresh, exact=True)
 
 
 @pytest.fixture(autouse=True)
@@ -26,42 +73,42 @@ def _threads():
     torch.set_num_threads(n)
 
 
-def test_origin_matrices_match_reference(kinova_chain):
-    g = load_golden("fk_known_answer.npz")
+def test_origin_matrices_match_reference(golden, kinova_chain):
+    g = golden.load("fk_known_answer.npz")
     for j, ref in zip(kinova_chain, g["origins"]):
-        _eq(O.origin_matrix(j.xyz, j.rpy).numpy(), ref)
+        golden.eq(O.origin_matrix(j.xyz, j.rpy).numpy(), ref)
 
 
 @pytest.mark.parametrize("b", range(4))
-def test_fk_batched_fp32_and_fp64(kinova_chain, b):
-    g = load_golden("fk_known_answer.npz")
+def test_fk_batched_fp32_and_fp64(golden, kinova_chain, b):
+    g = golden.load("fk_known_answer.npz")
     q32 = torch.from_numpy(g["q32"])
     base = torch.from_numpy(g["bases"][b])
-    _eq(O.ee_world(kinova_chain, q32, base).numpy(), g[f"ee32_b{b}"])
-    _eq(O.ee_world(kinova_chain, q32.double(), base.double()).numpy(), g[f"ee64_b{b}"])
+    golden.eq(O.ee_world(kinova_chain, q32, base).numpy(), g[f"ee32_b{b}"])
+    golden.eq(O.ee_world(kinova_chain, q32.double(), base.double()).numpy(), g[f"ee64_b{b}"])
 
 
 @pytest.mark.parametrize("b", range(4))
-def test_fk_single_host_path(kinova_chain, b):
-    g = load_golden("fk_known_answer.npz")
+def test_fk_single_host_path(golden, kinova_chain, b):
+    g = golden.load("fk_known_answer.npz")
     q32 = torch.from_numpy(g["q32"])
     base = torch.from_numpy(g["bases"][b])
     got = np.stack([O.ee_world_single(kinova_chain, q32[0, j], base).numpy() for j in range(4)])
-    _eq(got, g[f"eecpu_b{b}"])
+    golden.eq(got, g[f"eecpu_b{b}"])
 
 
-def test_rotation_utils():
-    g = load_golden("rotations.npz")
-    _eq(O.quat_xyzw_matrix(torch.from_numpy(g["quat"])).numpy(), g["quat_R"])
-    _eq(O.euler_zyx(torch.from_numpy(g["mats"])).numpy(), g["euler"])
-    _eq(O.quat_xyzw_matrix(torch.tensor([-0.5, -0.5, 0.5, -0.5])).numpy(), g["target_R"])
+def test_rotation_utils(golden):
+    g = golden.load("rotations.npz")
+    golden.eq(O.quat_xyzw_matrix(torch.from_numpy(g["quat"])).numpy(), g["quat_R"])
+    golden.eq(O.euler_zyx(torch.from_numpy(g["mats"])).numpy(), g["euler"])
+    golden.eq(O.quat_xyzw_matrix(torch.tensor([-0.5, -0.5, 0.5, -0.5])).numpy(), g["target_R"])
 
 
-def test_savgol():
-    g = load_golden("savgol.npz")
+def test_savgol(golden):
+    g = golden.load("savgol.npz")
     for key in [k for k in g if k.startswith("x_")]:
         H, A, W, P = map(int, key.split("_")[1:])
-        _eq(O.savgol(torch.from_numpy(g[key]), W, P).numpy(), g["y" + key[1:]])
+        golden.eq(O.savgol(torch.from_numpy(g[key]), W, P).numpy(), g["y" + key[1:]])
     # coefficients recovered from the reference's impulse response
     for key in [k for k in g if k.startswith("coef_")]:
         W, P = map(int, key.split("_")[1:])
@@ -74,91 +121,91 @@ def test_savgol_rejects_short_sequences():
 
 
 @pytest.mark.parametrize("name", ["drone_k128_h20.npz", "drone_k256_h32.npz"])
-def test_drone_steps(name):
-    g = load_golden(name)
+def test_drone_steps(golden, name):
+    g = golden.load(name)
     H = int(g["H"])
     for s in range(int(g["steps"])):
         r = O.drone_step(g[f"s{s}_x_in"], g[f"s{s}_v_in"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
                          torch.from_numpy(g[f"s{s}_noise"]), g["target"])
         for k in ("traj", "S", "w", "w_eps_raw", "w_eps", "u_prev_out", "x_out", "v_out"):
-            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+            golden.eq(r[k].numpy(), g[f"s{s}_{k}"])
         assert r["u_prev_out"].shape == (H, 3)
 
 
-def test_drone_noise_reproduces_reference_randn():
+def test_drone_noise_reproduces_reference_randn(golden):
     """torch.manual_seed(seed) + randn + Sigma reproduces the recorded noise."""
-    g = load_golden("drone_k128_h20.npz")
+    g = golden.load("drone_k128_h20.npz")
     torch.manual_seed(100)
     eps = O.draw_noise(128, 20, torch.from_numpy(g["sigma"]))
-    _eq(eps.numpy(), g["s0_noise"])
+    golden.eq(eps.numpy(), g["s0_noise"])
 
 
 @pytest.mark.parametrize("name", ["arm_k32_h32_f32.npz", "arm_k32_h32_f64.npz", "arm_k100_h32_f64.npz",
                                   "arm_k32_h32_gap.npz"])
-def test_arm_steps(kinova_chain, name):
-    g = load_golden(name)
+def test_arm_steps(golden, kinova_chain, name):
+    g = golden.load(name)
     f64 = bool(g["state_f64"])
     for s in range(int(g["steps"])):
         r = O.arm_step(kinova_chain, g["q_full"], g["v_full"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
                        torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"], f64=f64)
         for k in ("v", "q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out"):
-            _eq(r[k].numpy(), g[f"s{s}_{k}"])
-        _eq(r["qdes"], g[f"s{s}_qdes"])
-        _eq(r["vdes"], g[f"s{s}_vdes"])
+            golden.eq(r[k].numpy(), g[f"s{s}_{k}"])
+        golden.eq(r["qdes"], g[f"s{s}_qdes"])
+        golden.eq(r["vdes"], g[f"s{s}_vdes"])
         assert r["reach"] == bool(g[f"s{s}_reach"])
 
 
 ALL_TERMS = O.CostTerms(enabled=("covar", "center", "jtraj", "action", "limit"))
 
 
-def test_arm_all_cost_terms(kinova_chain):
+def test_arm_all_cost_terms(golden, kinova_chain):
     """F7: every CostManager term the reference leaves disabled, switched on
     (covar, centering, joint tracking, action, joint limit; cost_manager.py:83-87),
     fp64 state near joint 6's limit so the 1e10 penalty hits some samples."""
-    g = load_golden("arm_k64_h32_allcosts.npz")
+    g = golden.load("arm_k64_h32_allcosts.npz")
     for s in range(int(g["steps"])):
         r = O.arm_step(kinova_chain, g["q_full"], g["v_full"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
                        torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"], f64=True,
                        terms=ALL_TERMS)
         for name in ("covar", "center", "jtraj", "action", "limit"):
-            _eq(r["terms"][name].numpy(), g[f"s{s}_term_{name}"])
+            golden.eq(r["terms"][name].numpy(), g[f"s{s}_term_{name}"])
         for k in ("q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out"):
-            _eq(r[k].numpy(), g[f"s{s}_{k}"])
-        _eq(r["qdes"], g[f"s{s}_qdes"])
+            golden.eq(r[k].numpy(), g[f"s{s}_{k}"])
+        golden.eq(r["qdes"], g[f"s{s}_qdes"])
         assert (g[f"s{s}_term_limit"] > 0).any() and (g[f"s{s}_term_limit"] == 0).any()
 
 
-def test_arm_noise_reproduces_reference_randn():
-    g = load_golden("arm_k32_h32_f32.npz")
+def test_arm_noise_reproduces_reference_randn(golden):
+    g = golden.load("arm_k32_h32_f32.npz")
     torch.manual_seed(300)
-    _eq(O.draw_noise(32, 32, torch.eye(7) * 0.1).numpy(), g["s0_noise"])
-    g = load_golden("arm_k32_h32_gap.npz")    # the sampler's Sigma set to 1.0 I
+    golden.eq(O.draw_noise(32, 32, torch.eye(7) * 0.1).numpy(), g["s0_noise"])
+    g = golden.load("arm_k32_h32_gap.npz")    # the sampler's Sigma set to 1.0 I
     torch.manual_seed(800)
-    _eq(O.draw_noise(32, 32, torch.from_numpy(g["sigma"])).numpy(), g["s0_noise"])
+    golden.eq(O.draw_noise(32, 32, torch.from_numpy(g["sigma"])).numpy(), g["s0_noise"])
 
 
-def test_gap_fixture_is_well_conditioned():
+def test_gap_fixture_is_well_conditioned(golden):
     """F2c exists so the arm path meets the plain 1e-4 rel bar end to end: its
     top-2 cost gap must be >= 20 lambda in every step."""
-    g = load_golden("arm_k32_h32_gap.npz")
+    g = golden.load("arm_k32_h32_gap.npz")
     assert np.all(g["top2_gap"] >= 20 * 0.1)
 
 
-def test_wholebody_steps(kinova_chain):
-    g = load_golden("wholebody_k32_h64.npz")
-    _eq(O.base_rpy_from_quat(g["base_quat"]).numpy(), g["base_rpy"])
+def test_wholebody_steps(golden, kinova_chain):
+    g = golden.load("wholebody_k32_h64.npz")
+    golden.eq(O.base_rpy_from_quat(g["base_quat"]).numpy(), g["base_rpy"])
     for s in range(int(g["steps"])):
         r = O.wholebody_step(kinova_chain, g[f"s{s}_x_in"], g[f"s{s}_vx_in"], g[f"s{s}_q_in"],
                              g[f"s{s}_qd_in"], g["base_rpy"], torch.from_numpy(g[f"s{s}_u_prev_in"]),
                              torch.from_numpy(g[f"s{s}_noise"]), g["target_pos"], g["target_quat"])
         for k in ("q_samples", "ee", "S", "w", "w_eps_raw", "w_eps", "u_prev_out",
                   "x_out", "v_out", "qdes", "vdes"):
-            _eq(r[k].numpy(), g[f"s{s}_{k}"])
+            golden.eq(r[k].numpy(), g[f"s{s}_{k}"])
 
 
-def test_shard_combine_equals_global_softmin():
+def test_shard_combine_equals_global_softmin(golden):
     """The §8e combine (any shard split) equals the global softmin-weighted sum."""
-    g = load_golden("drone_k256_h32.npz")
+    g = golden.load("drone_k256_h32.npz")
     S = torch.from_numpy(g["s1_S"])
     eps = torch.from_numpy(g["s1_noise"])
     ref = torch.from_numpy(g["s1_w_eps_raw"]).double()
