@@ -938,7 +938,8 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
         const size_t nwaves = (size_t)e->V * nb * (e->threads / 64);
         if (hipMalloc(&e->d_stamps, nwaves * kStamps * 8) == hipSuccess) p.stamps = e->d_stamps;
         e->stamp_sum.assign(kStamps, 0.0);
-        (void)hipMalloc(&e->d_fstamps, (size_t)e->V * e->A * ((H + 7) / 8) * kStamps * 8);
+        // FINAL's blocks, then a shard's PACK blocks (mppi_debug_fstamps)
+        (void)hipMalloc(&e->d_fstamps, 2 * (size_t)e->V * e->A * ((H + 7) / 8) * kStamps * 8);
         e->fstamp_sum.assign(kStamps, 0.0);
     }
 #endif
@@ -1254,6 +1255,7 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         FinParams f = e->fp;
         pack_fields(e, f);
         f.tail = e->d_tail + kTailPack;
+        if (f.stamps) f.stamps += (size_t)e->V * e->A * e->fin_ts * kStamps;   // diagnostics: PACK's own blocks
         block_records(e, f);
         rc = mppi_launch_finalize(&f, e->stream);
         if (rc != 0) return fail(MPPI_ERR_HIP, "pack launch failed (%d)", rc);
@@ -1555,6 +1557,13 @@ mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us
 mppi_status mppi_synchronize(mppi_engine* e) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
+    // The last finalised step's completion flag is polled first (mapped host memory, a
+    // few hundred ns behind the kernel); hipStreamSynchronize alone wakes the host
+    // microseconds after the stream drains, which a short timed batch pays in full.
+    if (e->out_pending && !e->event_wait) {
+        mppi_status st = wait_outputs(e);
+        if (st != MPPI_OK) return st;
+    }
     HIP_TRY(hipStreamSynchronize(e->stream));
     return MPPI_OK;
 }
@@ -1660,6 +1669,21 @@ int64_t mppi_debug_stamps(mppi_engine* e, unsigned long long* out, int64_t max_w
         hipMemcpy(out, e->d_stamps, (size_t)nwaves * kStamps * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return MPPI_ERR_HIP;
     return nwaves;
+}
+
+// Diagnostic (MPPI_STAMPS builds): the raw stamps of the last FINAL (which = 0) or PACK
+// (which = 1) launch, kStamps uint64 per (vehicle, dim, t-slice) block.  Returns the block count.
+int64_t mppi_debug_fstamps(mppi_engine* e, unsigned long long* out, int64_t max_blocks, int32_t which) {
+    if (!e || !out || which < 0 || which > 1) return MPPI_ERR_INVALID_ARG;
+    if (!e->d_fstamps) return 0;
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const int64_t nb = (int64_t)e->V * e->A * e->fin_ts;
+    const int64_t n = std::min<int64_t>(max_blocks, nb);
+    if (hipStreamSynchronize(e->stream) != hipSuccess ||
+        hipMemcpy(out, e->d_fstamps + (size_t)which * nb * kStamps, (size_t)n * kStamps * 8, hipMemcpyDeviceToHost) !=
+            hipSuccess)
+        return MPPI_ERR_HIP;
+    return n;
 }
 
 int32_t mppi_philox_words(int32_t A) {

@@ -36,7 +36,7 @@ constexpr int kMaxRec = 4096;
 #define MPPI_FIN_XCDS 8
 #endif
 
-#ifdef MPPI_STAMPS
+#if defined(MPPI_STAMPS) && !defined(MPPI_TIMELINE)
 #define FSTAMP(i)                                                                    \
     do {                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                           \
@@ -45,8 +45,18 @@ constexpr int kMaxRec = 4096;
                 __builtin_amdgcn_s_memtime();                                        \
         __builtin_amdgcn_sched_barrier(0);                                           \
     } while (0)
+#define FSTAMPRT(i) do { } while (0)
+#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: block start / end (wave 0) in wall-clock time
+#define FSTAMP(i) do { } while (0)
+#define FSTAMPRT(i)                                                                  \
+    do {                                                                             \
+        if (pk.stamps && threadIdx.x == 0)                                           \
+            pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + (i)] =               \
+                __builtin_amdgcn_s_memrealtime();                                    \
+    } while (0)
 #else
 #define FSTAMP(i) do { } while (0)
+#define FSTAMPRT(i) do { } while (0)
 #endif
 
 // Block = 8 waves.  Lane (g, q) of wave wv holds window column q (CW = 16/32/64
@@ -88,33 +98,30 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // which one L2 then fetches once instead of once per slice.  Blocks b mod 8 >= X and
     // dims >= A exit at once.
     const int x8 = blockIdx.x & 7, j8 = blockIdx.x >> 3, na = (A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS;
-    const int sl = j8 / na, a = x8 + MPPI_FIN_XCDS * (j8 - sl * na), v = blockIdx.y;
+    // (na is 1 for A <= 8 and 2 for the whole-body's 10 dims: the general scalar division is
+    // ~30 dependent SALU ops at the head of every block)
+    const int sl = (na == 1) ? j8 : (na == 2) ? (j8 >> 1) : j8 / na;
+    const int a = x8 + MPPI_FIN_XCDS * (j8 - sl * na), v = blockIdx.y;
     if (x8 >= MPPI_FIN_XCDS || a >= A) return;
     if (MPPI_FIN_KO & 16) { if (tid == 0) p.u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
+    FSTAMPRT(13);
     FSTAMP(0);
     const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
     const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
     const float* hdr = hdr_base + (size_t)v * (uint32_t)hdr_vs;
     const float* col = dat_base + (size_t)v * (uint32_t)d_vs + (size_t)a * d_as + w0;
     const FinTail& T = *tail;
-    float* up = T.u_prev + (size_t)v * H * A;
     const int g = lane / CW, q = lane - g * CW, gr = wv * ROWS + g;
     const bool qv = q < W;
-    // wave 0 prefetches u_prev over the window (lane q <-> t = w0 + q), incl. the OLD
-    // u_prev[0] (mppi.py:157)
-    const float u_old = (wv == 0 && q < W && g == 0) ? up[(w0 + q) * A + a] : 0.0f;
-    // and the vehicle constants the outputs need (slice 0 of each dim, lane 0)
-    float x0f = 0.0f, v0f = 0.0f;
+    // wave 0's u_prev over the window (lane q <-> t = w0 + q, incl. the OLD u_prev[0],
+    // mppi.py:157) and the vehicle constants of the outputs (slice 0 of each dim, lane 0) are
+    // loaded AFTER the first chunk of record loads is issued (pin_tail below): they need the
+    // tail's pointers (an s_load round trip, then their own), and issued first they held the
+    // record loads behind both -- the register allocator paired a pending u_prev/vc load with
+    // the record offsets, and the whole wave waited for vmcnt(0) before its first record load
+    float u_old = 0.0f, x0f = 0.0f, v0f = 0.0f;
     double x0d = 0.0, v0d = 0.0;
-    if (tid == 0 && sl == 0) {
-        // vector loads (a VGPR offset the compiler cannot prove uniform): scalar loads of
-        // these fields were waited for on the spot, two dependent s_load round trips
-        // ahead of the record loads
-        int vz;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-        const VehicleConst* vcp = T.vc + v + vz;
-        x0f = vcp->pos0f[a]; v0f = vcp->vel0f[a]; x0d = vcp->pos0[a]; v0d = vcp->vel0[a];
-    }
+    float* up = nullptr;
 
     // The tail's parameters (FinTail), read into SGPRs while the record loads fly: left to
     // the compiler, each was an s_load waited for on the spot in wave 0's tail (15 serial
@@ -126,6 +133,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     float *wraw = nullptr, *wsmooth = nullptr, *u0p = nullptr, *stats = nullptr;
     double* outp = nullptr;
     uint32_t* flags = nullptr;
+    const VehicleConst* vcb = nullptr;
     float sg[WIN > 0 ? WIN : 1];
     auto pin_tail = [&]() {
         // every load issues first, then two empty asms consume them (one wait): pinned one
@@ -133,18 +141,30 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         coef = T.coef; dt = T.dt; dt2 = T.dt2;
         mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
         wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
+        up = T.u_prev; vcb = T.vc;
         if constexpr (WIN > 0) {
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
         }
         asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
                           "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
-                          "+s"(outp), "+s"(flags));
+                          "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb));
         if constexpr (WIN == 9)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
                               "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
         else if constexpr (WIN == 5)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]));
+        // then the loads that need those pointers (global address space: a flat load also
+        // counts in lgkmcnt, so every later scalar wait would wait for it too)
+        up += (size_t)v * H * A;
+        using gfloat = const __attribute__((address_space(1))) float;
+        using gdouble = const __attribute__((address_space(1))) double;
+        if (wv == 0 && q < W && g == 0) u_old = *(gfloat*)(up + (w0 + q) * A + a);
+        if (tid == 0 && sl == 0) {
+            const VehicleConst* vcp = vcb + v;
+            x0f = *(gfloat*)(vcp->pos0f + a); v0f = *(gfloat*)(vcp->vel0f + a);
+            x0d = *(gdouble*)(vcp->pos0 + a); v0d = *(gdouble*)(vcp->vel0 + a);
+        }
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
     // column of a row group, so each lane carries them and the wave fold runs over row groups
@@ -165,7 +185,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
             xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
         }
-        if (base == 0 && !(MPPI_FIN_KO & 64)) pin_tail();   // (64: timing knockout, tail parameters not loaded)
+        if (base == 0 && !(MPPI_FIN_KO & 64)) {   // (64: timing knockout, tail parameters not loaded)
+            __builtin_amdgcn_sched_barrier(0);   // the first chunk's record loads issue first
+            pin_tail();
+        }
 #pragma unroll
         for (int i = 0; i < kNPT; ++i)
             if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
@@ -232,17 +255,24 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int t = w0 + lane;              // this lane's time index (lanes < W)
     const bool own = lane < W && t >= t_lo && t < t_hi;
     if (mode == 1) {   // PACK raw sums into this shard's exchange slot
-        float* dst = T.dst + (size_t)v * T.P;
+        // the slot fields in one scalar round trip (each was its own wait in the tail)
+        float* dst = T.dst;
+        float* xbase = T.xbase;
+        int64_t xslot = T.xslot;
+        int32_t nslots = T.nslots, myslot = T.myslot, P = T.P;
+        asm volatile("" : "+s"(dst), "+s"(xbase), "+s"(xslot), "+s"(nslots), "+s"(myslot), "+s"(P));
+        dst += (size_t)v * P;
         if (a == 0 && sl == 0 && lane == 0) {
             dst[0] = rho; dst[1] = eta; dst[2] = eta2; dst[3] = nanf;
         }
         if (own) dst[kHdr + a * H + t] = N;
-        for (int s = 0; s < T.nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
-            if (s == T.myslot) continue;
-            float* z = T.xbase + (size_t)s * T.xslot + (size_t)v * T.P;
+        for (int s = 0; s < nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
+            if (s == myslot) continue;
+            float* z = xbase + (size_t)s * xslot + (size_t)v * P;
             if (a == 0 && sl == 0 && lane < kHdr) z[lane] = 0.0f;
             if (own) z[kHdr + a * H + t] = 0.0f;
         }
+        FSTAMPRT(14);
         return;
     }
 
@@ -327,6 +357,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         }
     }
     FSTAMP(6);
+    FSTAMPRT(14);
 }
 
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only

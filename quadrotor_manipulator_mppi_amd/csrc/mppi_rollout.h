@@ -388,7 +388,7 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 // =============================================================================
 // Diagnostic phase stamps (build with -DMPPI_STAMPS; see tools/stamps.md):
 // s_memtime per wave between scheduling barriers.  Compiled out otherwise.
-#ifdef MPPI_STAMPS
+#if defined(MPPI_STAMPS) && !defined(MPPI_TIMELINE)
 #define STAMP(i)                                                                                      \
     do {                                                                                              \
         __builtin_amdgcn_sched_barrier(0);                                                            \
@@ -418,6 +418,20 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
                                                (unsigned)__builtin_amdgcn_s_getreg(0xF804);           \
         }                                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
+#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: wave start / end in wall-clock time only (no phase stamps,
+                             // no waits: the kernel's own schedule)
+#define STAMP(i) do { } while (0)
+#define STAMPW(i) do { } while (0)
+#define STAMPRT(i)                                                                                    \
+    do {                                                                                              \
+        if (pk.stamps && lane == 0) {                                                                 \
+            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
+            if ((i) == 13)                                                                            \
+                pk.stamps[w_ * kStamps + 15] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
+                                               (unsigned)__builtin_amdgcn_s_getreg(0xF804);           \
+        }                                                                                             \
     } while (0)
 #else
 #define STAMP(i) do { } while (0)
