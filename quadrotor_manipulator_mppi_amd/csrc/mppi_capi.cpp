@@ -324,6 +324,8 @@ struct mppi_engine {
     uint32_t seq_ctr = 0;               // last completion-flag value handed out: monotonic and
                                         // independent of step_ctr (mppi_set_step_counter rewinds that)
     bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
+    bool no_flag_dbg = false;           // MPPI_DEBUG_NO_FLAG=1 (diagnostics, with MPPI_EVENT_WAIT=1): no step
+                                        // writes the completion flag, so the last step runs like the others
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
     float* d_S = nullptr;
@@ -960,6 +962,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.out_dim = e->out_dim;
     if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
     e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
+    e->no_flag_dbg = e->event_wait && getenv("MPPI_DEBUG_NO_FLAG") && atoi(getenv("MPPI_DEBUG_NO_FLAG")) != 0;
     f.stamps = e->d_fstamps;
     {   // the finalize's tail parameters, one device copy per launch kind (constant for the
         // engine's life): the control step's FINAL, a shard's PACK, and FINAL into the device
@@ -1271,8 +1274,9 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // no completion flag (and no fence) for unread steps
-    if (record_out) {   // a fresh value per read step, never 0 (the flags start zeroed): the flags
-                        // the previous read step left can never satisfy this step's wait
+    if (record_out && !e->no_flag_dbg) {   // a fresh value per read step, never 0 (the flags start zeroed):
+                                           // the flags the previous read step left can never satisfy this
+                                           // step's wait
         f.seq = ++e->seq_ctr;
         if (f.seq == 0u) f.seq = ++e->seq_ctr;
     }

@@ -46,14 +46,20 @@ constexpr int kMaxRec = 4096;
         __builtin_amdgcn_sched_barrier(0);                                           \
     } while (0)
 #define FSTAMPRT(i) do { } while (0)
-#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: block start / end (wave 0) in wall-clock time
-#define FSTAMP(i) do { } while (0)
+#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: block start / end (wave 0) in wall-clock time, the
+                             // XCD in slot 15, the first chunk's loads issued + tail pinned (slot 7)
+                             // and the wave fold's end (slot 1: records combined)
 #define FSTAMPRT(i)                                                                  \
     do {                                                                             \
-        if (pk.stamps && threadIdx.x == 0)                                           \
+        if (pk.stamps && threadIdx.x == 0) {                                         \
             pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + (i)] =               \
                 __builtin_amdgcn_s_memrealtime();                                    \
+            if ((i) == 13)                                                           \
+                pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + 15] =            \
+                    (unsigned long long)__builtin_amdgcn_s_getreg(0xF814);           \
+        }                                                                            \
     } while (0)
+#define FSTAMP(i) do { if ((i) == 1 || (i) == 7) FSTAMPRT(i); } while (0)
 #else
 #define FSTAMP(i) do { } while (0)
 #define FSTAMPRT(i) do { } while (0)
@@ -171,19 +177,33 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // only.  eta in fp32, like the reference's torch.sum of the fp32 exponentials
     // (mppi.py:184-188): <= 16 terms per lane, then 2 + 3 (8 waves) folds.
     float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f, eta = 0.0f, eta2 = 0.0f;
+    // Record loads through buffer resources over this vehicle's headers and this (dim,
+    // window)'s body columns: each load is one 32-bit VGPR offset (a full-rate add per row)
+    // instead of a 64-bit address (v_mad_u64_u32 + v_lshl_add_u64, both quarter-rate: ~380
+    // cycles of address math ahead of the first load).  Rows past n are masked at use (okm);
+    // their offsets run past the resources' ranges, which read 0 instead of faulting.
+    const uint32_t hrs_b = (uint32_t)hdr_rs * 4u, drs_b = (uint32_t)d_rs * 4u;
+    const __amdgpu_buffer_rsrc_t hrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hdr), 0, (int)((uint32_t)n * hrs_b), 0x00020000);
+    // (the range is block-uniform, but its W reaches the compiler through VGPR math: without
+    // readfirstlane every body load became a waterfall loop over a "divergent" resource)
+    const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(col), 0, __builtin_amdgcn_readfirstlane((int)((uint32_t)(n - 1) * drs_b + (uint32_t)W * 4u)),
+        0x00020000);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     for (int base = 0; base < n; base += TR * kNPT) {
         float4 hd[kNPT];
         float xv[kNPT];
-        uint32_t okm = 0;   // rows past n load row 0 and are masked at use: a select on the
-                            // loaded value here made the compiler wait for each load in turn
+        uint32_t okm = 0;   // rows past n are masked at use: a select on the loaded value
+                            // here made the compiler wait for each load in turn
+        const uint32_t r0 = (uint32_t)(base + gr);
+        const uint32_t hoff = r0 * hrs_b, coff = r0 * drs_b + (uint32_t)(qv ? q : 0) * 4u;
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
-            const int r = base + gr + i * TR;
-            const bool ok = r < n;
-            okm |= (uint32_t)ok << i;
-            const uint32_t rr = (uint32_t)(ok ? r : 0);   // 32-bit offsets (nrec <= 4096)
-            hd[i] = *reinterpret_cast<const float4*>(hdr + rr * (uint32_t)hdr_rs);
-            xv[i] = col[rr * (uint32_t)d_rs + (uint32_t)(qv ? q : 0)];
+            okm |= (uint32_t)(r0 + (uint32_t)(i * TR) < (uint32_t)n) << i;
+            const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(hrsrc, (int)(hoff + (uint32_t)(i * TR) * hrs_b), 0, 0);
+            hd[i] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
+            xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crsrc, (int)(coff + (uint32_t)(i * TR) * drs_b), 0, 0));
         }
         if (base == 0 && !(MPPI_FIN_KO & 64)) {   // (64: timing knockout, tail parameters not loaded)
             __builtin_amdgcn_sched_barrier(0);   // the first chunk's record loads issue first

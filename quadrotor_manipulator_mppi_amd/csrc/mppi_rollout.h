@@ -419,10 +419,18 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
         }                                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                            \
     } while (0)
-#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: wave start / end in wall-clock time only (no phase stamps,
-                             // no waits: the kernel's own schedule)
-#define STAMP(i) do { } while (0)
-#define STAMPW(i) do { } while (0)
+#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: wall-clock time at wave start / end and at three phase
+                             // boundaries (after the first group's Philox: slot 10, after the
+                             // prologue's barrier: slot 1, after the rollout groups: slot 5), no
+                             // waits: the kernel's own schedule
+#define STAMP(i)                                                                                      \
+    do {                                                                                              \
+        if (((i) == 1 || (i) == 5 || (i) == 10) && pk.stamps && lane == 0) {                          \
+            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
+        }                                                                                             \
+    } while (0)
+#define STAMPW(i) STAMP(i)
 #define STAMPRT(i)                                                                                    \
     do {                                                                                              \
         if (pk.stamps && lane == 0) {                                                                 \
@@ -636,7 +644,6 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // phases); the joint table and (V > 1) the vehicle block go to LDS.
     __shared__ JointDev jnt[kMaxJ];
     __shared__ VehicleConst vcv;
-    __shared__ unsigned rmin_bits;   // block min of the waves' rho (costs >= 0: uint order = float order)
     const DevParams& p = pk;
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;   // block size as a preloaded argument: blockDim would be an implicit-argument s_load
@@ -667,7 +674,6 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // in SGPRs spills): V == 1 from the kernel arguments, else from vc[v]
     constexpr int kVCW = (int)(sizeof(VehicleConst) / 4);
     const int vcr = (tid < kVCW) ? (VONE ? ((const int*)&pk.vc0)[tid] : ((const int*)(pk.vc + v))[tid]) : 0;
-    if (tid == 0) rmin_bits = 0x7F800000u;   // +inf
     // touch every kernel-argument line the hot phases read (one s_load per 64 B): they
     // land in the scalar cache while the first group's Philox draw runs below
     // (an integer fold: uniform, so SALU -- a float sum took one VALU op per line)
@@ -1132,15 +1138,14 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     STAMP(5);
 
     // ---- cross-wave combine in LDS -> one partial record per block, one barrier:
-    //      rho_b via an LDS atomic min before the deposit; every record thread
-    //      rescales the 8 wave slots itself (f_w = exp(-(rho_w - rho_b)/lambda)).
+    //      after the barrier every record thread takes rho_b = min of the 8 wave slots'
+    //      rho and rescales them itself (f_w = exp(-(rho_w - rho_b)/lambda)).
     //      LDS: [8][4 + NCH*64*NA]; every lane (all R segments) deposits acc
     float* wsh = smem + ((HA + 3) & ~3);           // always 8 wave slots (unrolled reads)
     const int wstride = kWs;   // >= 4 + NCH*64*NA (the integrator's buffer may be larger)
     float* mine = wsh + wid * wstride;
     if (lane == 0) {
         mine[0] = rho_w; mine[1] = eta_w; mine[2] = eta2_w; mine[3] = nan_w ? 1.0f : 0.0f;
-        if (rho_w < INFINITY) atomicMin(&rmin_bits, __float_as_uint(rho_w));
     }
     for (int i = nw * wstride + tid; i < 8 * wstride; i += nthr)   // absent waves: rho = inf, acc = 0
         wsh[i] = ((i - nw * wstride) % wstride == 0) ? INFINITY : 0.0f;
@@ -1151,13 +1156,17 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     STAMPW(11);
     lds_barrier();
     STAMP(6);
-    const float rho_b = __uint_as_float(rmin_bits);
-    float fw[8];
+    // rho_b = the min of the 8 wave slots, which every thread reads for f_w anyway (an LDS
+    // atomicMin before the barrier cost a waterfall loop and a ds_min per wave)
+    float rws[8], rho_b = INFINITY;
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
-        const float rw = wsh[w * wstride];
-        fw[w] = (rw < INFINITY) ? __expf(p.coef * (rw - rho_b)) : 0.0f;
+        rws[w] = wsh[w * wstride];
+        rho_b = fminf(rho_b, rws[w]);
     }
+    float fw[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) fw[w] = (rws[w] < INFINITY) ? __expf(p.coef * (rws[w] - rho_b)) : 0.0f;
     STAMP(12);
     if (tid == 0) {
         float eta = 0.0f, eta2 = 0.0f, nanf = 0.0f;
