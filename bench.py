@@ -246,16 +246,18 @@ def reduce_max(vals, dist, device):
 def timed_batches(run, n_batches, barrier):
     """The contract's timed region, repeated: each batch is EXACTLY `steps` control steps
     bracketed by barrier + synchronize on both sides (wall clock); returns the per-batch
-    seconds.  The line's ms_per_step is the median batch / steps (a 20-step batch is
-    ~0.2 ms, so one host hiccup at a bracket would otherwise set the number)."""
-    out = []
+    seconds and the host time each batch's enqueue took (when that is close to the batch,
+    the step was host-bound).  The line's ms_per_step is the median batch / steps (a 20-step
+    batch is ~0.2 ms, so one host hiccup at a bracket would otherwise set the number)."""
+    out, enq = [], []
     for _ in range(n_batches):
         barrier()
         t0 = time.perf_counter()
         run()
+        enq.append(time.perf_counter() - t0)   # host time to enqueue the batch (diagnostic)
         barrier()
         out.append(time.perf_counter() - t0)
-    return out
+    return out, enq
 
 
 def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1):
@@ -308,7 +310,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
             tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
         se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
         barrier()
-    bt = timed_batches(lambda: se.run_steps(steps_n), batches, barrier)
+    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier)
     bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
     if tim is not None and dist is not None:   # the slowest rank's kernels
         tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
@@ -327,7 +329,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.native else None
-    res = {"batches_s": bt, "dt": float(np.median(bt)), "tim": tim, "lat": lat, "K": eng.K, "H": eng.H,
+    res = {"batches_s": bt, "enqueue_s": benq, "dt": float(np.median(bt)), "tim": tim, "lat": lat, "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
            "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native,
            "native_error": se.native_error, "world": world,
@@ -420,6 +422,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                                    else "1 GPU")},
         "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
+                   "enqueue_ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r.get("enqueue_s", [])],
                    "basis": "median over the batches; each batch = exactly `steps` control steps bracketed by "
                             "barrier + synchronize (wall clock), max over ranks"},
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
@@ -477,6 +480,8 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the event-timed kernel loops (profiler runs: the trace then holds only the "
                          "control steps); no roofline in the line")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="leave the process's CPU affinity alone (default: bind to the GPU's local CPUs)")
     ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
@@ -486,6 +491,14 @@ def main():
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+
+    # the launching process on the GPU's own socket (quadrotor_manipulator_mppi_amd.affinity):
+    # from the other socket the host side of a step costs more than the GPU side
+    binding = None
+    if not args.no_numa_bind:
+        from quadrotor_manipulator_mppi_amd.affinity import bind_to_gpu_numa
+        binding = bind_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
+        log(f"cpu binding: {binding}")
 
     import torch
     launched = "WORLD_SIZE" in os.environ
@@ -530,7 +543,9 @@ def main():
         if world == 1 and r["tim"] is not None:
             measured = measured_hbm(local)
             log(f"measured HBM: {measured}")
-        print(json.dumps(make_line(workload, r, args, secondary, cpu, cpu_all, measured)), file=json_out, flush=True)
+        line = make_line(workload, r, args, secondary, cpu, cpu_all, measured)
+        line["host_binding"] = binding
+        print(json.dumps(line), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

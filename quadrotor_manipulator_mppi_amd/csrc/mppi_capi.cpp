@@ -326,6 +326,8 @@ struct mppi_engine {
     bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
     bool no_flag_dbg = false;           // MPPI_DEBUG_NO_FLAG=1 (diagnostics, with MPPI_EVENT_WAIT=1): no step
                                         // writes the completion flag, so the last step runs like the others
+    int out_dbg = 0;                    // MPPI_DEBUG_OUT (diagnostics): 1 = unread steps write their outputs
+                                        // to device scratch, 2 = mppi_kernel_timing writes to mapped host memory
     float* d_traj = nullptr;
     float* d_noise_out = nullptr;
     float* d_S = nullptr;
@@ -963,6 +965,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
     e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
     e->no_flag_dbg = e->event_wait && getenv("MPPI_DEBUG_NO_FLAG") && atoi(getenv("MPPI_DEBUG_NO_FLAG")) != 0;
+    e->out_dbg = getenv("MPPI_DEBUG_OUT") ? atoi(getenv("MPPI_DEBUG_OUT")) : 0;
     f.stamps = e->d_fstamps;
     {   // the finalize's tail parameters, one device copy per launch kind (constant for the
         // engine's life): the control step's FINAL, a shard's PACK, and FINAL into the device
@@ -1281,6 +1284,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
         if (f.seq == 0u) f.seq = ++e->seq_ctr;
     }
     final_records(e, f);
+    if (e->out_dbg == 1 && !record_out) f.tail = e->d_tail + kTailScratch;   // diagnostic (MPPI_DEBUG_OUT)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
     int rc = mppi_launch_finalize(&f, e->stream);
@@ -1455,6 +1459,7 @@ mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us,
     f.wraw = nullptr;
     f.wsmooth = nullptr;
     f.tail = e->d_tail + kTailScratch;   // (the same outputs, from the kernel's device-resident copy)
+    if (e->out_dbg == 2) f.tail = e->d_tail + kTailFinal;   // diagnostic: outputs into mapped host memory
     float ms0 = 0.0f, ms1 = 0.0f, ms2 = 0.0f;
     int rc = 0;
 #define KT_TRY(expr)                                                                        \

@@ -17,6 +17,7 @@ import bench
 def _fake_result(world, rank, model="wholebody", K=8192, H=64, native=False, backend="gloo"):
     rng = np.random.default_rng(rank)
     return {"batches_s": list(20 * 20e-6 * (1 + 0.05 * rng.random(7)) * (1 + rank)), "dt": None,
+            "enqueue_s": list(20 * 8e-6 * np.ones(7)),
             "tim": {"rollout_us": 12.5 + rank, "finalize_us": 4.8, "pair_us": 17.4 + rank,
                     "rollout_in_step_us": 12.6 + rank, "method": "fake"},
             "lat": [3e-5] * 10, "K": K, "H": H, "A": 10, "V": 1, "strong": True,
