@@ -492,14 +492,6 @@ def main():
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
 
-    # the launching process on the GPU's own socket (quadrotor_manipulator_mppi_amd.affinity):
-    # from the other socket the host side of a step costs more than the GPU side
-    binding = None
-    if not args.no_numa_bind:
-        from quadrotor_manipulator_mppi_amd.affinity import bind_to_gpu_numa
-        binding = bind_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
-        log(f"cpu binding: {binding}")
-
     import torch
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -507,6 +499,13 @@ def main():
     workload = args.workload or ("c4" if launched else "arm_c3")
     # ranks beyond the visible devices wrap (rehearsing N ranks on fewer GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    # the launching thread on the GPU's own socket (quadrotor_manipulator_mppi_amd.affinity);
+    # threads created later (the CPU baseline's pool) inherit it
+    binding = None
+    if not args.no_numa_bind:
+        from quadrotor_manipulator_mppi_amd.affinity import bind_to_gpu_numa
+        binding = bind_to_gpu_numa(local)
+        log(f"cpu binding: {binding}")
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -6,13 +6,13 @@ link when the launching thread runs on the other socket from the GPU, and the ho
 of a step then costs more than the GPU side (measured on the MI355X boxes: 8-11 us of
 host enqueue per step from a remote socket against ~6 us from the GPU's own socket, with
 a ~9.8 us GPU step).  ``bind_to_gpu_numa`` restricts the calling process to the CPUs the
-kernel lists as PCIe-local to the HIP device (``/sys/bus/pci/devices/<bdf>/local_cpulist``),
+kernel lists as PCIe-local to the HIP device (``/sys/bus/pci/devices/<bdf>/local_cpulist``;
+Linux binds the calling thread, and the threads it creates afterwards inherit the mask),
 the usual binding of a GPU-driving process.  It does nothing where the information is
 missing (no sysfs entry, a one-socket host) and never widens the current affinity.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 from typing import List, Optional
 
@@ -31,19 +31,17 @@ def _parse_cpulist(s: str) -> List[int]:
 
 
 def gpu_pci_bus_id(device: int = 0) -> Optional[str]:
-    """The HIP device's PCI address ("0000:75:00.0"), from hipDeviceGetPCIBusId."""
-    for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
-        try:
-            hip = ctypes.CDLL(name)
-            break
-        except OSError:
-            hip = None
-    if hip is None:
+    """The HIP device's PCI address ("0000:75:00.0"), from torch's device properties (the
+    process's one HIP runtime: loading libamdhip64 a second time, e.g. through ctypes, can
+    hand torch a different runtime than the one it ships with)."""
+    try:
+        import torch
+        if not torch.cuda.is_available() or device >= torch.cuda.device_count():
+            return None
+        pr = torch.cuda.get_device_properties(device)
+        return f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+    except Exception:   # no GPU, an old torch without the fields
         return None
-    buf = ctypes.create_string_buffer(64)
-    if hip.hipDeviceGetPCIBusId(buf, ctypes.c_int(64), ctypes.c_int(device)) != 0:
-        return None
-    return buf.value.decode().lower()
 
 
 def gpu_local_cpus(device: int = 0) -> Optional[List[int]]:

@@ -42,9 +42,17 @@ def main():
     eng.synchronize()
     pairs = [eng.kernel_timing_ex(200)[2] for _ in range(5)]
     rows = []
+    pause = float(os.environ.get("MPPI_PROBE_PAUSE_MS", "0")) * 1e-3   # host pause after each batch's sync
+    spin = float(os.environ.get("MPPI_PROBE_SPIN_MS", "0")) * 1e-3     # host busy loop after each batch's sync
     for _ in range(12):
         eng.synchronize()
         torch.cuda.synchronize()
+        if pause:
+            time.sleep(pause)
+        if spin:   # busy host before the batch (CPU frequency hypothesis)
+            t_end = time.perf_counter() + spin
+            while time.perf_counter() < t_end:
+                pass
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(se.stream)
@@ -58,6 +66,8 @@ def main():
     a = np.array(rows)
     print(json.dumps({"workload": name, "steps": steps, "MPPI_DEBUG_OUT": os.environ.get("MPPI_DEBUG_OUT", "0"),
                       "cpus": os.environ.get("MPPI_PROBE_CPUS", "default"), "ncpus": len(os.sched_getaffinity(0)),
+                      "pause_ms": pause * 1e3, "spin_ms": spin * 1e3,
+                      "enqueue_batches": [round(x, 2) for x in a[:, 1]],
                       "pair_us": round(float(np.median(pairs)), 3),
                       "run_steps_gpu_us": round(float(np.median(a[:, 0])), 3),
                       "run_steps_enqueue_us": round(float(np.median(a[:, 1])), 3),
