@@ -243,7 +243,7 @@ def reduce_max(vals, dist, device):
     return [float(x) for x in t.tolist()]
 
 
-def timed_batches(run, n_batches, barrier):
+def timed_batches(run, n_batches, barrier, prime=None):
     """The contract's timed region, repeated: each batch is EXACTLY `steps` control steps
     bracketed by barrier + synchronize on both sides (wall clock); returns the per-batch
     seconds and the host time each batch's enqueue took (when that is close to the batch,
@@ -251,6 +251,8 @@ def timed_batches(run, n_batches, barrier):
     batch is ~0.2 ms, so one host hiccup at a bracket would otherwise set the number)."""
     out, enq = [], []
     for _ in range(n_batches):
+        if prime is not None:   # the warmup steps, untimed, ahead of every batch (not only the first)
+            prime()
         barrier()
         t0 = time.perf_counter()
         run()
@@ -310,7 +312,11 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
             tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
         se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
         barrier()
-    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier)
+    # every batch follows its own W untimed warmup steps (the contract's warmup, repeated per
+    # batch): the host's launch rate after a pause is what a batch then measures less of
+    # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
+    prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
+    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
     bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
     if tim is not None and dist is not None:   # the slowest rank's kernels
         tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
@@ -423,8 +429,8 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
                    "enqueue_ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r.get("enqueue_s", [])],
-                   "basis": "median over the batches; each batch = exactly `steps` control steps bracketed by "
-                            "barrier + synchronize (wall clock), max over ranks"},
+                   "basis": "median over the batches; each batch = `warmup` untimed steps, then exactly `steps` "
+                            "control steps bracketed by barrier + synchronize (wall clock), max over ranks"},
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
         "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
         "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
