@@ -31,13 +31,6 @@ constexpr int kMaxRec = 4096;
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
-// completion-flag protocol (k_finalize tail): 1 = system-scope release fence (L2 writeback)
-// before the flag; 0 = only wait for the output stores' acknowledgment -- measured UNSAFE:
-// 3 of 9000 stressed control calls read outputs their flags did not cover
-// (tests/test_gpu_flag.py, profiles/r03/flag_protocol_stress.txt).  Kept for that test only.
-#ifndef MPPI_FLAG_WBL2
-#define MPPI_FLAG_WBL2 1
-#endif
 // XCDs the finalize's blocks run on (8; 4 = the first four, see the block map in k_finalize)
 #ifndef MPPI_FIN_XCDS
 #define MPPI_FIN_XCDS 8
@@ -378,15 +371,14 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs).
         // seq == 0: nobody waits on this step (mppi_run_steps before its last step) -- no
         // system-scope fence, whose L2 writeback costs ~1.5 us of kernel time.  A read step
-        // needs it even though the outputs are in fine-grained (coherent) host memory: the
-        // acknowledgment of this thread's stores alone did not order them before the flag
-        // (MPPI_FLAG_WBL2 above).
+        // needs it although the outputs are in fine-grained (coherent) host memory, and it is
+        // the cheapest correct protocol measured (tests/test_gpu_flag.py stress,
+        // profiles/r03/flag_protocol_stress.txt): waiting only for the plain output stores'
+        // acknowledgment let 3 of 9000 calls read outputs their flag did not cover, and
+        // system-scope output stores (written through, acknowledged from the host) plus that
+        // wait were correct but 2 us slower per control call.
         if (seq != 0u) {
-            if (MPPI_FLAG_WBL2) {
-                __threadfence_system();
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            __threadfence_system();
             __hip_atomic_store(flags + (size_t)v * A + a, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
