@@ -23,7 +23,8 @@
 // Timing knockouts for tools/ experiments only (MPPI_HIPCC_EXTRA=-DMPPI_KO=n; results are
 // wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain,
 // 8 the pose cost, 16 the trajectory stores, 32 Box-Muller, 64 the block record body,
-// 128 the u_prev loads (H*A <= 4 * block threads).
+// 128 the u_prev loads (H*A <= 4 * block threads), 256 the prologue's block barrier (LDS
+// staging read unsynchronised).
 #ifndef MPPI_KO
 #define MPPI_KO 0
 #endif
@@ -718,7 +719,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         if (VONE && blockIdx.x == 0) ((int*)pk.vc)[i] = x;
     }
     STAMPW(8);
-    lds_barrier();
+    if (!(MPPI_KO & 256)) lds_barrier();
     const VehicleConst& vc = vcv;
     const float* sdiag = pk.sdiag;
     const int H = H_arg, K = pk.K;
