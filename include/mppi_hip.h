@@ -258,8 +258,14 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
 /* n back-to-back asynchronous control steps (rollout + finalize each, device
  * noise, state and warm start resident on the GPU); single-shard engines, or
  * shards with an engine-owned communicator (rollout, all-reduce, finalize).
- * No host synchronisation: pair with mppi_synchronize / mppi_read_outputs. */
+ * No host synchronisation: pair with mppi_synchronize / mppi_read_outputs.
+ * Single-shard engines dispatch the steps natively: raw AQL packets on an HSA queue the
+ * engine owns, the kernels from the library's code objects, their arguments resident in
+ * device memory (MPPI_DISPATCH = auto (default) | aql (required) | hip). */
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
+
+/* How the last mppi_run_steps was dispatched: "aql", or "hip: <why not native>". */
+mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len);
 
 mppi_status mppi_synchronize(mppi_engine* e);
 

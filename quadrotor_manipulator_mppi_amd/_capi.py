@@ -104,6 +104,7 @@ PROTOTYPES = {
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),
     "mppi_step": (_ST, [_P, _D, _F, _D, _F, C.POINTER(Stats)]),
     "mppi_run_steps": (_ST, [_P, C.c_int32]),
+    "mppi_dispatch_info": (_ST, [_P, C.c_char_p, C.c_int32]),
     "mppi_synchronize": (_ST, [_P]),
     "mppi_get_costs": (_ST, [_P, _F]),
     "mppi_get_weights": (_ST, [_P, _F]),

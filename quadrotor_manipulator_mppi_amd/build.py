@@ -33,8 +33,18 @@ _ASAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-po
 _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
 SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
            ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=14"]),
-           ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", [])]
-HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", os.path.join("..", "..", "include", "mppi_hip.h")]
+           ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
+HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",
+           os.path.join("..", "..", "include", "mppi_hip.h")]
+# Native dispatch (mppi_aql.cpp) loads each kernel unit's gfx950 code object from next to the
+# library: <library stem>.<unit>.co, built from the same source with the same flags.
+KERNEL_UNITS = [s for s, _ in SOURCES if s.endswith(".hip")]
+
+
+def code_object_path(lib: str, unit: str) -> str:
+    return os.path.splitext(lib)[0] + "." + os.path.splitext(unit)[0] + ".co"
+
+
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 EXTRA = os.environ.get("MPPI_HIPCC_EXTRA", "").split()   # experiment flags (tools/), empty in production
 
@@ -48,6 +58,8 @@ def hipcc() -> str:
 
 def _stale() -> bool:
     if not os.path.exists(LIB):
+        return True
+    if not all(os.path.exists(code_object_path(LIB, u)) for u in KERNEL_UNITS):
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, s) for s, _ in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS] + \
@@ -67,7 +79,7 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False, stamp
         (["-DMPPI_STAMPS"] if stamps else []) + (_ASAN if asan else []) + EXTRA
     objdir = os.path.join(LIB_DIR, "obj" + ("_stamps" if stamps else "_asan" if asan else ""))
     os.makedirs(objdir, exist_ok=True)
-    objs, procs = [], []
+    objs, procs, cos = [], [], []
     for src, flags in SOURCES:   # compile the translation units in parallel
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
         cmd = base + flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
@@ -75,13 +87,24 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False, stamp
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
         objs.append(obj)
+        if src in KERNEL_UNITS and not asan:   # the same unit's device code alone, for native dispatch
+            co = code_object_path(out, src)
+            cmd = base + flags + ["--cuda-device-only", "-c", "--no-gpu-bundle-output", "-o", co + ".tmp",
+                                  os.path.join(CSRC, src)]
+            procs.append((src + " (code object)", subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                                                   text=True)))
+            cos.append(co)
     for src, pr in procs:
         so, se = pr.communicate()
         if pr.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src} ({pr.returncode}):\n{so}\n{se}")
         if verbose and se.strip():
             print(se)
+    for co in cos:
+        os.replace(co + ".tmp", co)
+    rocm_lib = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + \
+        ["-L", rocm_lib, "-lhsa-runtime64"] + \
         (["-Xarch_host", "-fsanitize=address", "-shared-libsan"] if asan else [])
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:

@@ -1,0 +1,363 @@
+// mppi_aql.cpp -- native dispatch of the control step: raw AQL kernel-dispatch packets on an
+// HSA queue of the engine's own (see mppi_aql.h).
+//
+// Why: hipLaunchKernel costs the host 2.4-3.3 us per launch on the MI355X boxes (kernel-
+// argument marshalling and a device-memory copy of the argument block each time), and a
+// (rollout, finalize) pair alternating 8-9 us (tools/microbench10.hip,
+// profiles/r03/microbench_aql_dispatch.txt) -- the same order as the GPU's 9.6 us C3 step,
+// so mppi_run_steps ran host-bound in some batches (profiles/r03/final_r03b: 5.2-8.2 us of
+// enqueue per step, 9.96-10.9 us per step).  Here the argument blocks are written once into
+// device memory; per step the host writes two 64 B packets into the queue's ring and stores
+// the doorbell: 0.57 us per pair, and the GPU side runs the dependent pair back to back.
+//
+// The kernels are the library's own: build.py writes each kernel translation unit's gfx950
+// code object next to the library (<library>.<unit>.co); they are loaded once per device
+// through the HSA loader, and a launch's symbol comes from the launcher itself (mppi_device.h
+// go(), capture mode), so native and HIP dispatch run the same code with the same arguments.
+#include "mppi_aql.h"
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <immintrin.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <atomic>
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local mppi::LaunchDesc* t_capture = nullptr;
+
+struct Kern {
+    uint64_t obj = 0;
+    uint32_t kas = 0, gss = 0, pss = 0;
+};
+
+// one device's loaded code objects (process-wide; executables live as long as the process)
+struct Device {
+    bool tried = false, ok = false;
+    std::string why;
+    hsa_agent_t agent{};
+    std::vector<hsa_executable_t> exes;
+    std::unordered_map<std::string, Kern> syms;
+};
+std::mutex g_mu;
+std::map<int, Device> g_dev;
+
+const char* const kUnits[] = {"mppi_rollout_drone", "mppi_rollout_arm", "mppi_rollout_arm32", "mppi_rollout_wb",
+                              "mppi_rollout_quad", "mppi_finalize"};
+
+std::string hsa_msg(hsa_status_t s) {
+    const char* m = nullptr;
+    if (hsa_status_string(s, &m) != HSA_STATUS_SUCCESS || !m) return "HSA status " + std::to_string((int)s);
+    return m;
+}
+
+struct AgentMatch {
+    uint32_t domain, bdf;
+    bool found;
+    hsa_agent_t agent;
+};
+hsa_status_t match_agent(hsa_agent_t a, void* data) {
+    auto* m = (AgentMatch*)data;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+        return HSA_STATUS_SUCCESS;
+    uint32_t bdf = 0, dom = 0;
+    if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS) dom = 0;
+    if (bdf == m->bdf && dom == m->domain && !m->found) { m->agent = a; m->found = true; }
+    return HSA_STATUS_SUCCESS;
+}
+
+// directory + stem of this library: the code objects sit next to it
+bool library_stem(std::string* stem) {
+    Dl_info info;
+    if (!dladdr((void*)&match_agent, &info) || !info.dli_fname) return false;
+    std::string p = info.dli_fname;
+    if (p.size() > 3 && p.compare(p.size() - 3, 3, ".so") == 0) p.resize(p.size() - 3);
+    *stem = p;
+    return true;
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    char buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, f)) > 0) out->insert(out->end(), buf, buf + r);
+    fclose(f);
+    return !out->empty();
+}
+
+// caller holds g_mu
+Device* device_for(int ordinal) {
+    Device& d = g_dev[ordinal];
+    if (d.tried) return &d;
+    d.tried = true;
+    char bus[64] = {0};
+    unsigned dom = 0, b = 0, dv = 0, fn = 0;
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, ordinal) != hipSuccess ||
+        sscanf(bus, "%x:%x:%x.%x", &dom, &b, &dv, &fn) != 4) {
+        d.why = "no PCI bus id for HIP device " + std::to_string(ordinal);
+        return &d;
+    }
+    hsa_status_t st = hsa_init();   // reference-counted: HIP initialised the runtime already
+    if (st != HSA_STATUS_SUCCESS) { d.why = "hsa_init: " + hsa_msg(st); return &d; }
+    AgentMatch m{dom, (b << 8) | (dv << 3) | fn, false, {}};
+    hsa_iterate_agents(match_agent, &m);
+    if (!m.found) { d.why = std::string("no HSA agent at ") + bus; return &d; }
+    d.agent = m.agent;
+    std::string stem;
+    if (!library_stem(&stem)) { d.why = "cannot locate the library's own path"; return &d; }
+    for (const char* u : kUnits) {
+        const std::string path = stem + "." + u + ".co";
+        std::vector<char> co;
+        if (!read_file(path, &co)) { d.why = "missing code object " + path + " (python -m quadrotor_manipulator_mppi_amd.build)"; return &d; }
+        hsa_code_object_reader_t rd;
+        hsa_executable_t ex;
+        if ((st = hsa_code_object_reader_create_from_memory(co.data(), co.size(), &rd)) != HSA_STATUS_SUCCESS ||
+            (st = hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &ex)) !=
+                HSA_STATUS_SUCCESS) {
+            d.why = "loading " + path + ": " + hsa_msg(st);
+            return &d;
+        }
+        // the reader's buffer must outlive the executable: keep it (process lifetime)
+        static std::vector<std::vector<char>> keep;
+        keep.push_back(std::move(co));
+        if ((st = hsa_executable_load_agent_code_object(ex, d.agent, rd, nullptr, nullptr)) != HSA_STATUS_SUCCESS ||
+            (st = hsa_executable_freeze(ex, nullptr)) != HSA_STATUS_SUCCESS) {
+            d.why = "loading " + path + ": " + hsa_msg(st);
+            return &d;
+        }
+        d.exes.push_back(ex);
+    }
+    d.ok = true;
+    return &d;
+}
+
+// caller holds g_mu
+bool lookup(Device* d, const char* name, Kern* k, std::string* err) {
+    std::string sym = std::string(name) + ".kd";
+    auto it = d->syms.find(sym);
+    if (it != d->syms.end()) { *k = it->second; return true; }
+    for (hsa_executable_t ex : d->exes) {
+        hsa_executable_symbol_t s;
+        if (hsa_executable_get_symbol_by_name(ex, sym.c_str(), &d->agent, &s) != HSA_STATUS_SUCCESS) continue;
+        Kern r;
+        if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &r.obj) != HSA_STATUS_SUCCESS ||
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &r.kas) != HSA_STATUS_SUCCESS ||
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &r.gss) != HSA_STATUS_SUCCESS ||
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &r.pss) != HSA_STATUS_SUCCESS)
+            break;
+        d->syms[sym] = r;
+        *k = r;
+        return true;
+    }
+    *err = "kernel " + sym + " not in the code objects";
+    return false;
+}
+
+}  // namespace
+
+extern "C" mppi::LaunchDesc* mppi_capture_target(void) { return t_capture; }
+
+namespace mppi_aql {
+
+constexpr uint32_t kQueueSize = 4096;   // packets (256 KB ring)
+constexpr size_t kArgSlot = 4096;       // bytes per argument block: [rollout | finalize]
+
+struct Step {
+    Device* dev = nullptr;
+    hsa_queue_t* q = nullptr;
+    hsa_signal_t done{0};                 // outstanding batches; each batch's last packet decrements it
+    std::atomic<int> qerr{0};             // HSA status of an asynchronous queue error
+    unsigned char* d_args = nullptr;      // device: rollout arguments at 0, finalize at kArgSlot
+    mppi::LaunchDesc roll{}, fin{};       // what the device blocks hold (step word as uploaded)
+    Kern kr, kf;
+    uint32_t step_off = 0, step_word = 0; // the resident rollout's dispatch-id relative step word
+    bool valid = false;
+    int64_t outstanding = 0;              // batches dispatched and not yet waited for
+};
+
+void set_capture(mppi::LaunchDesc* d) { t_capture = d; }
+
+static void queue_error(hsa_status_t status, hsa_queue_t*, void* data) {
+    ((Step*)data)->qerr.store((int)status);
+}
+
+Step* step_create(int device, std::string* why) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Device* d = device_for(device);
+    if (!d->ok) { *why = d->why; return nullptr; }
+    Step* s = new Step();
+    s->dev = d;
+    hsa_status_t st = hsa_queue_create(d->agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, queue_error, s, UINT32_MAX,
+                                       UINT32_MAX, &s->q);
+    if (st != HSA_STATUS_SUCCESS) { *why = "hsa_queue_create: " + hsa_msg(st); delete s; return nullptr; }
+    if ((st = hsa_signal_create(0, 0, nullptr, &s->done)) != HSA_STATUS_SUCCESS) {
+        *why = "hsa_signal_create: " + hsa_msg(st);
+        hsa_queue_destroy(s->q);
+        delete s;
+        return nullptr;
+    }
+    if (hipMalloc(&s->d_args, 2 * kArgSlot) != hipSuccess) {
+        *why = "hipMalloc of the argument blocks failed";
+        hsa_signal_destroy(s->done);
+        hsa_queue_destroy(s->q);
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+void step_destroy(Step* s) {
+    if (!s) return;
+    std::string e;
+    if (s->outstanding) step_wait(s, 60000, &e);
+    hsa_signal_destroy(s->done);
+    hsa_queue_destroy(s->q);
+    (void)hipFree(s->d_args);
+    delete s;
+}
+
+bool step_busy(Step* s) { return s && s->outstanding > 0; }
+
+// a launch's argument block against the kernel's: only explicit arguments (no hidden ones),
+// LDS within the CU's 160 KB.  (Scratch: the packet carries the kernel's private segment size;
+// the runtime backs the queue's scratch on demand, as for HIP's own queues.)
+static bool check_launch(const mppi::LaunchDesc& l, const Kern& k, std::string* err) {
+    if (k.kas < l.arg_bytes || k.kas - l.arg_bytes >= 16 || k.kas > kArgSlot) {
+        *err = std::string(l.symbol) + ": kernel-argument segment " + std::to_string(k.kas) + " B vs " +
+               std::to_string(l.arg_bytes) + " B packed";
+        return false;
+    }
+    if (k.gss + l.lds > 160 * 1024) { *err = std::string(l.symbol) + ": LDS over 160 KB"; return false; }
+    for (int i = 0; i < 3; ++i)
+        if (l.grid[i] == 0 || l.block[i] == 0) { *err = std::string(l.symbol) + ": empty grid"; return false; }
+    if ((uint64_t)l.block[0] * l.block[1] * l.block[2] > 1024) { *err = "block over 1024 threads"; return false; }
+    return true;
+}
+
+static bool same_launch(const mppi::LaunchDesc& a, const mppi::LaunchDesc& b, uint32_t skip_off) {
+    if (strcmp(a.symbol, b.symbol) != 0 || memcmp(a.grid, b.grid, sizeof a.grid) != 0 ||
+        memcmp(a.block, b.block, sizeof a.block) != 0 || a.lds != b.lds || a.arg_bytes != b.arg_bytes)
+        return false;
+    if (skip_off + 4 > a.arg_bytes) return memcmp(a.args, b.args, a.arg_bytes) == 0;
+    return memcmp(a.args, b.args, skip_off) == 0 &&
+           memcmp(a.args + skip_off + 4, b.args + skip_off + 4, a.arg_bytes - skip_off - 4) == 0;
+}
+
+int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
+                 uint32_t step_off, std::string* err) {
+    // the next rollout's packet index (the queue holds (rollout, finalize) pairs only, so
+    // rollouts sit at indices of one parity and (index >> 1) counts pairs)
+    const uint32_t word = step - (uint32_t)(hsa_queue_load_write_index_relaxed(s->q) >> 1);
+    if (s->valid && s->step_word == word && s->step_off == step_off && same_launch(roll, s->roll, step_off) &&
+        same_launch(fin, s->fin, ~0u))
+        return 0;
+    Kern kr, kf;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
+    }
+    if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
+    if (step_off + 4 > roll.arg_bytes) { *err = "step counter outside the rollout's arguments"; return -2; }
+    // the queue may still be reading the blocks about to be overwritten
+    if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
+    std::vector<unsigned char> h(2 * kArgSlot, 0);
+    memcpy(h.data(), roll.args, roll.arg_bytes);
+    memcpy(h.data() + step_off, &word, 4);
+    memcpy(h.data() + kArgSlot, fin.args, fin.arg_bytes);
+    if (hipMemcpy(s->d_args, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        *err = "uploading the argument blocks failed";
+        s->valid = false;
+        return -1;
+    }
+    s->roll = roll;
+    s->fin = fin;
+    s->kr = kr;
+    s->kf = kf;
+    s->step_off = step_off;
+    s->step_word = word;
+    s->valid = true;
+    return 0;
+}
+
+// One kernel-dispatch packet: body first, then header + setup in one release store (the
+// packet processor may read the slot as soon as the header says KERNEL_DISPATCH).
+static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l, void* args, hsa_signal_t sig,
+                       bool system_release) {
+    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
+    auto* p = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & (q->size - 1));
+    p->workgroup_size_x = (uint16_t)l.block[0];
+    p->workgroup_size_y = (uint16_t)l.block[1];
+    p->workgroup_size_z = (uint16_t)l.block[2];
+    p->reserved0 = 0;
+    p->grid_size_x = l.grid[0] * l.block[0];
+    p->grid_size_y = l.grid[1] * l.block[1];
+    p->grid_size_z = l.grid[2] * l.block[2];
+    p->private_segment_size = k.pss;
+    p->group_segment_size = k.gss + l.lds;
+    p->kernel_object = k.obj;
+    p->kernarg_address = args;
+    p->reserved2 = 0;
+    p->completion_signal = sig;
+    // each kernel waits for the one before (barrier bit) and sees its writes (agent-scope
+    // acquire); the batch's last one releases to system scope (the outputs in host memory)
+    const uint16_t header =
+        (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+                   (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                   ((system_release ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT)
+                    << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+    const uint32_t setup = 3u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    __atomic_store_n((uint32_t*)p, (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
+}
+
+int step_dispatch(Step* s, int n, std::string* err) {
+    if (!s->valid) { *err = "step_dispatch before step_prepare"; return -1; }
+    if (n <= 0) return 0;
+    if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
+    hsa_signal_add_relaxed(s->done, 1);   // this batch's completion
+    ++s->outstanding;
+    const hsa_signal_t none{0};
+    void* ra = s->d_args;
+    void* fa = s->d_args + kArgSlot;
+    for (int i = 0; i < n; ++i) {
+        const bool last = i == n - 1;
+        put(s->q, s->kr, s->roll, ra, none, false);
+        put(s->q, s->kf, s->fin, fa, last ? s->done : none, last);
+        // the doorbell takes the index of the last packet written
+        hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
+    }
+    return 0;
+}
+
+int step_wait(Step* s, int timeout_ms, std::string* err) {
+    if (!s || !s->outstanding) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (hsa_signal_load_scacquire(s->done) == 0) break;
+        if (s->qerr.load()) {
+            *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load());
+            return -1;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+            *err = "native dispatch: no completion after " + std::to_string(timeout_ms) + " ms";
+            return -1;
+        }
+        _mm_pause();
+    }
+    s->outstanding = 0;
+    return 0;
+}
+
+}  // namespace mppi_aql

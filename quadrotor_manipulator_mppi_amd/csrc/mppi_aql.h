@@ -1,0 +1,46 @@
+// mppi_aql.h -- native dispatch of the control step (mppi_aql.cpp).  Internal.
+//
+// mppi_run_steps' (rollout, finalize) pairs as raw AQL kernel-dispatch packets on an HSA
+// queue the engine owns, instead of one hipLaunchKernel per kernel: the kernels come from
+// the library's own gfx950 code objects (lib/<library>.<unit>.co, loaded through the HSA
+// loader), their argument blocks live in device memory and are written only when their
+// content changes.  The rollout's Philox step counter -- the one argument that changes every
+// step -- is passed relative to the dispatch id (the packet's index in the queue, which the
+// waves receive in SGPRs): step = arg + (id >> 1), the queue holding (rollout, finalize)
+// pairs only.  The host's work per step is two 64 B packets and a doorbell store.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+#include "mppi_dev.h"
+
+namespace mppi_aql {
+
+struct Step;   // one engine's queue, completion signal and device-resident argument blocks
+
+// nullptr (and why) when native dispatch is unavailable on this device ordinal.
+Step* step_create(int device, std::string* why);
+void step_destroy(Step* s);
+
+// Make the device-resident argument blocks hold these two launches such that the next
+// rollout dispatched runs step `step`: the rollout's step word (byte offset step_off of its
+// arguments, dispatch-id relative) becomes step - (next packet index >> 1).  Uploads only when
+// a launch differs from the resident one (the step word excluded) or the resident step word
+// would not give `step`; waits for the queue to drain before overwriting.  0; -2 when the launches
+// cannot be dispatched natively (a symbol the code objects lack, hidden arguments);
+// -1 on a runtime failure (*err says why).
+int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
+                 uint32_t step_off, std::string* err);
+// n (rollout, finalize) pairs, each kernel dependent on the one before; the last finalize
+// carries the completion signal and a system-scope release.
+int step_dispatch(Step* s, int n, std::string* err);
+// Until every dispatched pair has completed.  -1 on a queue error or after timeout_ms.
+int step_wait(Step* s, int timeout_ms, std::string* err);
+bool step_busy(Step* s);
+
+// Install (or, with nullptr, remove) the calling thread's capture target: the launchers then
+// describe their launch into it instead of launching (mppi_device.h go()).
+void set_capture(mppi::LaunchDesc* d);
+
+}  // namespace mppi_aql

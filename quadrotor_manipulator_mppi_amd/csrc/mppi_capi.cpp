@@ -20,6 +20,7 @@
 #include <thread>
 #include <vector>
 
+#include "mppi_aql.h"
 #include "mppi_dev.h"
 
 using namespace mppi;
@@ -365,6 +366,13 @@ struct mppi_engine {
     int64_t stamp_n = 0;
     double clk_sum = 0.0;
     int64_t roll_n = 0, fin_n = 0;
+    // native dispatch of mppi_run_steps (mppi_aql.cpp): MPPI_DISPATCH = hip | aql | auto (default)
+    mppi_aql::Step* aql = nullptr;
+    int aql_mode = 2;                   // 0 hip, 1 aql (required), 2 auto (aql when available)
+    bool aql_tried = false;             // step_create attempted (its failure is final for the engine)
+    bool aql_off = false;               // this engine's launches are not dispatchable natively
+    std::string aql_why = "no mppi_run_steps yet";   // why the last run went through HIP ("" = native)
+    bool aql_out = false;               // the pending outputs come from a native batch
 };
 
 namespace {
@@ -420,9 +428,19 @@ size_t traj_floats(const mppi_engine* e) {   // all vehicles' planes
     return (size_t)e->V * e->C * plane;
 }
 
+// Native batches are not ordered with the engine's HIP stream: every entry point that touches
+// the device (use_device) first waits for them.
+mppi_status aql_join(mppi_engine* e) {
+    if (e->aql && mppi_aql::step_busy(e->aql)) {
+        std::string err;
+        if (mppi_aql::step_wait(e->aql, 60000, &err) != 0) return fail(MPPI_ERR_HIP, "%s", err.c_str());
+    }
+    return MPPI_OK;
+}
+
 mppi_status use_device(mppi_engine* e) {
     HIP_TRY(hipSetDevice(e->cfg.device));
-    return MPPI_OK;
+    return aql_join(e);
 }
 
 size_t off_u0(const mppi_engine* e) { return ((size_t)e->V * e->out_dim * sizeof(double) + 15) & ~size_t(15); }
@@ -966,6 +984,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
     e->no_flag_dbg = e->event_wait && getenv("MPPI_DEBUG_NO_FLAG") && atoi(getenv("MPPI_DEBUG_NO_FLAG")) != 0;
     e->out_dbg = getenv("MPPI_DEBUG_OUT") ? atoi(getenv("MPPI_DEBUG_OUT")) : 0;
+    if (const char* d = getenv("MPPI_DISPATCH")) e->aql_mode = !strcmp(d, "hip") ? 0 : !strcmp(d, "aql") ? 1 : 2;
     f.stamps = e->d_fstamps;
     {   // the finalize's tail parameters, one device copy per launch kind (constant for the
         // engine's life): the control step's FINAL, a shard's PACK, and FINAL into the device
@@ -1007,6 +1026,7 @@ void mppi_destroy(mppi_engine* e) {
         (void)hipFree(e->d_fstamps);
     }
     (void)hipSetDevice(e->cfg.device);
+    if (e->aql) mppi_aql::step_destroy(e->aql);   // waits for its last batch
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto& pr : e->roll_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1294,6 +1314,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     if (record_out) HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
     ++e->step_ctr;
     e->out_pending = record_out;
+    e->aql_out = false;
     return MPPI_OK;
 }
 
@@ -1309,6 +1330,7 @@ mppi_status mppi_finalize(mppi_engine* e) {
 // one queue packet).  The event stays the backstop: it is queried every few
 // hundred polls, which also surfaces a faulted queue as an error.
 static mppi_status wait_outputs(mppi_engine* e) {
+    if (e->aql_out) return aql_join(e);   // a native batch: its completion signal (system-scope release)
     if (!e->event_wait) {
         const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
         const int n = e->V * e->A;
@@ -1415,10 +1437,90 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
     return mppi_read_outputs(e, out, u0, stats);
 }
 
+// why this engine's mppi_run_steps cannot go native (nullptr: it can)
+static const char* aql_ineligible(const mppi_engine* e) {
+    if (e->aql_mode == 0) return "MPPI_DISPATCH=hip";
+    if (sharded(e)) return "sharded step (its collective runs on the HIP stream)";
+    if (e->timing) return "per-launch timing events (mppi_enable_timing)";
+    if (e->d_stamps) return "stamps diagnostics";
+    if (e->out_dbg || e->no_flag_dbg) return "output diagnostics";
+    return nullptr;
+}
+
+// The rollout's step counter word: its third argument (seed_lo, seed_hi, step, ...), the same
+// position in k_rollout and k_rollout_quad (mppi_rollout.h, mppi_rollout_quad.hip).  Under
+// native dispatch it is relative to the dispatch id (kNoiseStepFromId in the noise-mode word).
+constexpr uint32_t kRollStepOff = 8;
+constexpr int32_t kNoiseStepFromId = 0x100;   // = mppi_device.h
+
+// n steps as native AQL packets (mppi_aql.cpp).  *used = false: the caller runs them through
+// HIP (auto mode, native dispatch unavailable for this engine; e->aql_why says why).
+static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
+    *used = false;
+    if (const char* why = aql_ineligible(e)) { e->aql_why = why; return MPPI_OK; }
+    if (e->aql_off) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    if (!e->aql) {
+        if (!e->aql_tried) {
+            e->aql_tried = true;
+            std::string why;
+            e->aql = mppi_aql::step_create(e->cfg.device, &why);
+            if (!e->aql) e->aql_why = why;
+        }
+        if (!e->aql) {
+            e->aql_off = true;
+            return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
+        }
+    }
+    // HIP work still queued on the engine's stream (uploads, an earlier HIP-path step) first
+    const hipError_t q = hipStreamQuery(e->stream);
+    if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(e->stream));
+    else if (q != hipSuccess) return fail(MPPI_ERR_HIP, "engine stream: %s", hipGetErrorString(q));
+    // the two launches exactly as the HIP path makes them, described instead of launched
+    static thread_local LaunchDesc roll, fin;
+    DevParams p = e->dp;
+    p.noise_in = nullptr;
+    p.vc0 = e->h_vc[0];
+    p.step_ctr = 0u;                      // (set by step_prepare: relative to the dispatch id)
+    p.noise_mode |= kNoiseStepFromId;
+    FinParams f = e->fp;
+    f.mode = 0;
+    f.seq = 0u;   // completion: the batch's signal, not a flag
+    final_records(e, f);
+    mppi_aql::set_capture(&roll);
+    int rc = mppi_launch_rollout(&p, e->threads, e->stream);
+    if (rc == 0) {
+        mppi_aql::set_capture(&fin);
+        rc = mppi_launch_finalize(&f, e->stream);
+    }
+    mppi_aql::set_capture(nullptr);
+    if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
+    std::string err;
+    const int pr = mppi_aql::step_prepare(e->aql, roll, fin, e->step_ctr, kRollStepOff, &err);
+    if (pr == -2) {   // not dispatchable natively (a kernel the code objects lack, hidden arguments)
+        e->aql_off = true;
+        e->aql_why = err;
+        return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", err.c_str()) : MPPI_OK;
+    }
+    if (pr != 0 || mppi_aql::step_dispatch(e->aql, n, &err) != 0)
+        return fail(MPPI_ERR_HIP, "native dispatch: %s", err.c_str());
+    e->step_ctr += (uint32_t)n;
+    e->out_pending = true;
+    e->aql_out = true;
+    e->aql_why.clear();
+    *used = true;
+    return MPPI_OK;
+}
+
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     if (!e || n < 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_run_steps: bad arguments");
     if (sharded(e) && !e->comm) return fail(MPPI_ERR_STATE, "mppi_run_steps on a shard needs mppi_comm_init");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_run_steps needs device noise");
+    if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_run_steps before mppi_set_state");
+    if (n == 0) return MPPI_OK;
+    bool used = false;
+    mppi_status st = run_steps_aql(e, n, &used);
+    if (st != MPPI_OK || used) return st;
     for (int i = 0; i < n; ++i) {
         mppi_status st = mppi_rollout(e, nullptr);
         if (st != MPPI_OK) return st;
@@ -1563,13 +1665,19 @@ mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us
     return st;
 }
 
+mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len) {
+    if (!e || !buf || len <= 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_dispatch_info: bad arguments");
+    snprintf(buf, (size_t)len, "%s%s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str());
+    return MPPI_OK;
+}
+
 mppi_status mppi_synchronize(mppi_engine* e) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
     // The last finalised step's completion flag is polled first (mapped host memory, a
     // few hundred ns behind the kernel); hipStreamSynchronize alone wakes the host
     // microseconds after the stream drains, which a short timed batch pays in full.
-    if (e->out_pending && !e->event_wait) {
+    if (e->out_pending && !e->event_wait && !e->aql_out) {
         mppi_status st = wait_outputs(e);
         if (st != MPPI_OK) return st;
     }

@@ -142,6 +142,20 @@ struct FinTail {
 };
 enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailSlots = 3 };
 
+// A kernel launch as data (mppi_aql.cpp): while a LaunchDesc is installed for the calling
+// thread (mppi_capture_target), the launchers fill it in instead of launching through HIP --
+// the kernel's symbol, grid, block, dynamic LDS and its argument block laid out as the
+// kernel-argument segment (each argument at its natural alignment, as the code object's
+// metadata lists them).
+struct LaunchDesc {
+    char symbol[192];
+    uint32_t grid[3];        // blocks per dimension
+    uint32_t block[3];       // threads per block
+    uint32_t lds;            // dynamic LDS bytes
+    uint32_t arg_bytes;
+    alignas(16) unsigned char args[2048];
+};
+
 // Finalize / pack kernel parameters.
 struct FinParams {
     int32_t model, V, H, A, nq, qoff, state_f64;
@@ -190,4 +204,6 @@ int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int
                         void* stream);
 int mppi_launch_philox(uint64_t seed, uint32_t step, int vehicle, int64_t k0, int K, int H, int A,
                        float* z, uint32_t* raw, void* stream);
+// the calling thread's capture target (null: launch through HIP); mppi_aql.cpp
+mppi::LaunchDesc* mppi_capture_target(void);
 }

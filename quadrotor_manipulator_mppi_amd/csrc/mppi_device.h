@@ -5,12 +5,29 @@
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <type_traits>
 
 #include "mppi_dev.h"
 
 using namespace mppi;
 
+// The dispatch id of the running kernel: the AQL packet's index in its queue, handed to the
+// waves in user SGPRs (no memory access).  The LLVM intrinsic by its name: clang has no
+// builtin for it.
+extern "C" __device__ uint64_t mppi_dispatch_id(void) __asm("llvm.amdgcn.dispatch.id");
+
 namespace {
+
+// noise-mode flag of native dispatch (mppi_aql.cpp): the rollout's step-counter argument is
+// relative to the dispatch id -- step = arg + (dispatch id >> 1) -- so one argument block,
+// written once, serves every (rollout, finalize) pair the engine's queue runs
+constexpr int32_t kNoiseStepFromId = 0x100;
+__device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg) {
+    return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
 // (lgkmcnt) but NOT for its outstanding global stores (vmcnt), which
@@ -100,6 +117,35 @@ __device__ __forceinline__ float wave_fold_all(float x, Op op) {
     x = op(x, dpp_all<0x141>(x));   // row_half_mirror
     x = op(x, dpp_all<0x140>(x));   // row_mirror
     return fold_rows<16>(x, op);
+}
+
+// ------------------------------------------------------------------ launches
+// Every launch of the control step goes through go(): through HIP, or -- while the calling
+// thread has a capture target (mppi_aql.cpp, native dispatch) -- described into it: the
+// symbol (namef fills it; the Itanium name of the instantiation, which the code object's
+// symbol table holds), the geometry, and the arguments converted to the kernel's parameter
+// types and laid out at their natural alignment, as the kernel-argument segment holds them.
+template <typename T>
+inline void pack_arg(unsigned char* buf, uint32_t& off, const T& v) {
+    off = (off + (uint32_t)alignof(T) - 1u) & ~((uint32_t)alignof(T) - 1u);
+    if (off + sizeof(T) <= sizeof(LaunchDesc::args)) memcpy(buf + off, &v, sizeof(T));
+    off += (uint32_t)sizeof(T);
+}
+template <typename NameF, typename... P, typename... Arg>
+inline int go(void (*k)(P...), NameF namef, dim3 grid, dim3 block, size_t lds, hipStream_t s, Arg... a) {
+    static_assert(sizeof...(P) == sizeof...(Arg), "one value per kernel parameter");
+    if (LaunchDesc* d = mppi_capture_target()) {
+        namef(d->symbol, sizeof(d->symbol));
+        d->grid[0] = grid.x; d->grid[1] = grid.y; d->grid[2] = grid.z;
+        d->block[0] = block.x; d->block[1] = block.y; d->block[2] = block.z;
+        d->lds = (uint32_t)lds;
+        uint32_t off = 0;
+        (pack_arg<std::decay_t<P>>(d->args, off, static_cast<std::decay_t<P>>(a)), ...);
+        d->arg_bytes = off;
+        return off <= sizeof(d->args) ? 0 : -1;
+    }
+    hipLaunchKernelGGL(k, grid, block, lds, s, a...);
+    return (int)hipGetLastError();
 }
 
 }  // namespace

@@ -409,9 +409,13 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
     const dim3 grid(8 * ((p->A + MPPI_FIN_XCDS - 1) / MPPI_FIN_XCDS) * p->ts, p->V), block(nt);   // XCD-aware map (k_finalize)
     hipStream_t s = (hipStream_t)stream;
 #define MPPI_FIN_GO(CWV, WINV, NTV)                                                                       \
-    hipLaunchKernelGGL((k_finalize<CWV, WINV, NTV>), grid, block, 0, s, p->hdr, p->dat, p->tail, nh, geo, \
-                       (int32_t)p->hdr_rs, (int32_t)p->d_rs, (int32_t)p->d_as, (int32_t)p->hdr_vs,    \
-                       (int32_t)p->d_vs, p->seq, *p)
+    return go(k_finalize<CWV, WINV, NTV>,                                                                 \
+              [](char* b, size_t n) {                                                                     \
+                  snprintf(b, n, "_Z10k_finalizeILi%dELi%dELi%dEEvPKfS1_PKN4mppi7FinTailEjjiiiiijNS2_9FinParamsE", \
+                           CWV, WINV, NTV);                                                               \
+              },                                                                                          \
+              grid, block, 0, s, p->hdr, p->dat, p->tail, nh, geo, (int32_t)p->hdr_rs, (int32_t)p->d_rs,   \
+              (int32_t)p->d_as, (int32_t)p->hdr_vs, (int32_t)p->d_vs, p->seq, *p)
 #define MPPI_FIN_LAUNCH(CWV, WINV)                                                                        \
     do {                                                                                                  \
         if (nt == 128) MPPI_FIN_GO(CWV, WINV, 128);                                                       \
@@ -430,7 +434,7 @@ extern "C" int mppi_launch_finalize(const FinParams* p, void* stream) {
 #undef MPPI_FIN_WIN
 #undef MPPI_FIN_LAUNCH
 #undef MPPI_FIN_GO
-    return (int)hipGetLastError();
+    return -1;
 }
 
 #ifdef MPPI_PROBE

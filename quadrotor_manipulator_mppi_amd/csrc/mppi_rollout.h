@@ -630,8 +630,8 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
 // latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
 __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
-                                                 const uint32_t step_ctr, const uint32_t k_off,
-                                                 const int32_t noise_mode, const int32_t H_arg,
+                                                 const uint32_t step_arg, const uint32_t k_off,
+                                                 const int32_t noise_arg, const int32_t H_arg,
                                                  const int32_t nthr,
                                                  const float* __restrict__ u_prev,
                                                  const JointDev* __restrict__ jtab, const DevParams pk) {
@@ -649,6 +649,8 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     const int v = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;   // block size as a preloaded argument: blockDim would be an implicit-argument s_load
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
+    const int32_t noise_mode = noise_arg & 0xFF;
+    const uint32_t step_ctr = step_of(step_arg, noise_arg);   // (native dispatch: from the dispatch id)
     STAMPRT(13);
     STAMP(0);
     // issue the global loads first (addresses need only preloaded scalars and the
@@ -1207,18 +1209,25 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
 // =============================================================================
 // launchers
 // =============================================================================
+// the instantiation's symbol (native dispatch looks it up in the code object)
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
+inline void rollout_symbol(char* buf, size_t n) {
+    snprintf(buf, n, "_Z9k_rolloutILi%dELi%dELi%dELi%dELb%dELb%dELb%dELb%dEEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE",
+             MODEL, NA, NCH, LSEG, (int)F64, (int)VONE, (int)XC, (int)ONEG);
+}
+
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
 inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>()) * sizeof(float);
     if (p.V == 1)
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>), dim3(p.nb, p.V), dim3(threads), lds,
-                           s, p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
-                           p.u_prev, p.joints, p);
-    else
-        hipLaunchKernelGGL((k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>), dim3(p.nb, p.V), dim3(threads), lds,
-                           s, p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads,
-                           p.u_prev, p.joints, p);
-    return (int)hipGetLastError();
+        return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>,
+                  rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
+                  p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads, p.u_prev,
+                  p.joints, p);
+    return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>,
+              rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
+              p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads, p.u_prev, p.joints,
+              p);
 }
 
 // the single-group (ONEG) variant exists for the common kernel at NCH == 1

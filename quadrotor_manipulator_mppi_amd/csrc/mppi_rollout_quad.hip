@@ -80,8 +80,8 @@ __device__ __forceinline__ float qsum(float x) {
 // (fewer records for the finalize: its record loop is sequential in chunks).
 template <bool VONE, bool LIT, int NWD, int NT>
 __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, const uint32_t seed_hi,
-                                                            const uint32_t step_ctr, const uint32_t k_off,
-                                                            const int32_t noise_mode, const int32_t H,
+                                                            const uint32_t step_arg, const uint32_t k_off,
+                                                            const int32_t noise_arg, const int32_t H,
                                                             const float* __restrict__ u_prev, const DevParams pk) {
     static_assert(NWD == 1 || NWD == kQWaves, "dynamics waves per block");
     static_assert(NT == kQThreads || (NWD == 1 && NT == kQThreadsWide), "block size");
@@ -94,6 +94,8 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     __shared__ float4 part[kQWaves][64];       // NWD > 1: the waves' record partials (lane = t)
     const DevParams& p = pk;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, v = blockIdx.y, b = blockIdx.x;
+    const int32_t noise_mode = noise_arg & 0xFF;
+    const uint32_t step_ctr = step_of(step_arg, noise_arg);   // (native dispatch: from the dispatch id)
     const int K = p.K;
     const int kb = b * QR;                       // the block's rollouts kb .. kb+QR-1
     float* const eps_t = qlds;
@@ -320,8 +322,13 @@ extern "C" int mppi_launch_rollout_quad(const DevParams* p, int threads, void* s
     hipStream_t s = (hipStream_t)stream;
     const bool wide = nwd == 1 && (size_t)p->nb * p->V <= 512;
 #define MPPI_QUAD_GO(VO, LI, NW, NT)                                                                             \
-    hipLaunchKernelGGL((k_rollout_quad<VO, LI, NW, NT>), dim3(p->nb, p->V), dim3(NT), lds, s, p->seed_lo,       \
-                       p->seed_hi, p->step_ctr, (uint32_t)p->k_offset, p->noise_mode, p->H, p->u_prev, *p)
+    return go(k_rollout_quad<VO, LI, NW, NT>,                                                                    \
+              [](char* b, size_t n) {                                                                            \
+                  snprintf(b, n, "_Z14k_rollout_quadILb%dELb%dELi%dELi%dEEvjjjjiiPKfN4mppi9DevParamsE", (int)VO, \
+                           (int)LI, NW, NT);                                                                     \
+              },                                                                                                 \
+              dim3(p->nb, p->V), dim3(NT), lds, s, p->seed_lo, p->seed_hi, p->step_ctr, (uint32_t)p->k_offset,   \
+              p->noise_mode, p->H, p->u_prev, *p)
 #define MPPI_QUAD_NW(VO, LI)                                                                                     \
     do {                                                                                                         \
         if (wide) MPPI_QUAD_GO(VO, LI, 1, kQThreadsWide);                                                        \
@@ -335,5 +342,5 @@ extern "C" int mppi_launch_rollout_quad(const DevParams* p, int threads, void* s
     }
 #undef MPPI_QUAD_NW
 #undef MPPI_QUAD_GO
-    return (int)hipGetLastError();
+    return -1;
 }

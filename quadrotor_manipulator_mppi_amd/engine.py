@@ -278,6 +278,12 @@ class Engine:
     def synchronize(self):
         capi.check(self._L.mppi_synchronize(self._h), "synchronize")
 
+    def dispatch_info(self) -> str:
+        """How the last run_steps was dispatched: "aql" (native packets) or "hip: <why>"."""
+        buf = C.create_string_buffer(256)
+        capi.check(self._L.mppi_dispatch_info(self._h, buf, len(buf)), "dispatch_info")
+        return buf.value.decode(errors="replace")
+
     def stats(self) -> List[StepStats]:
         st = self._stats
         return [StepStats(s.rho, s.eta, s.ess, bool(s.nonfinite), bool(s.reach))

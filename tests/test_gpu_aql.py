@@ -1,0 +1,131 @@
+"""Native dispatch (csrc/mppi_aql.cpp): mppi_run_steps as raw AQL packets on the engine's own
+HSA queue must compute exactly what the HIP launches compute -- the same kernels (loaded
+from the library's code objects), the same arguments (captured from the launchers), the
+Philox step counter advanced on the device by the finalize.  Every case runs one engine per
+dispatch mode on identical inputs and compares bit for bit: u_prev, the outputs, the costs,
+and the step after (a HIP-path control call must continue the native counter)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HOME = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]
+
+
+def _state(model, V=1, shift=0.0):
+    if model == "arm":
+        s = [0, 0, 1, 0, 0, 0, 1] + HOME + [0.0] * 7
+    elif model == "drone":
+        s = [0.0, 0.0, 1.0, 0.0, 0.0, 0.0]
+    elif model == "quadrotor":
+        s = [0.0, 0.0, 1.0, 0.0, 0.0, 0.0] + [0.0] * 6
+    else:
+        s = [0, 0, 1, 0, 0, 0, 1] + HOME + [0.0] * 10
+    s = np.tile(np.array(s, np.float64), (V, 1))
+    s[:, 0] += shift
+    return s
+
+
+def _pair(monkeypatch, model, **kw):
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    engines = []
+    for mode in ("hip", "aql"):
+        monkeypatch.setenv("MPPI_DISPATCH", mode)   # read at mppi_create
+        e = Engine(make_config(model, device=0, seed=11, **kw))
+        for v in range(e.V):
+            if model in ("drone", "quadrotor"):
+                e.set_target([1.0, 2.0, 3.4], vehicle=v)
+            else:
+                e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5], vehicle=v)
+        e.set_state(_state(model, e.V))
+        engines.append(e)
+    monkeypatch.delenv("MPPI_DISPATCH")
+    return engines
+
+
+def _same(h, a, what):
+    h.synchronize()
+    a.synchronize()
+    assert a.dispatch_info() == "aql", a.dispatch_info()
+    assert h.dispatch_info().startswith("hip"), h.dispatch_info()
+    np.testing.assert_array_equal(a.get_u_prev(), h.get_u_prev(), err_msg=what + ": u_prev")
+    np.testing.assert_array_equal(a.get_costs(), h.get_costs(), err_msg=what + ": costs")
+    oh, uh, sh = h.read_outputs()
+    oa, ua, sa = a.read_outputs()
+    np.testing.assert_array_equal(oa, oh, err_msg=what + ": outputs")
+    np.testing.assert_array_equal(ua, uh, err_msg=what + ": u0")
+    assert [s.rho for s in sa] == [s.rho for s in sh] and [s.eta for s in sa] == [s.eta for s in sh], what
+
+
+CASES = [
+    ("arm", dict(n_samples=4096, n_horizon=32)),                       # C3 (fp64 state)
+    ("arm", dict(n_samples=1024, n_horizon=32, state_f64=False)),
+    ("arm", dict(n_samples=2048, n_horizon=100)),                      # 2 chunks per rollout
+    ("arm", dict(n_samples=512, n_horizon=32, n_vehicles=4)),          # fleet (vehicle block in memory)
+    ("drone", dict(n_samples=4096, n_horizon=32)),
+    ("wholebody", dict(n_samples=8192, n_horizon=64)),                 # the C4 shard shape, one group per wave
+    ("wholebody", dict(n_samples=32768, n_horizon=64)),                # several groups per wave
+    ("quadrotor", dict(n_samples=1024, n_horizon=32)),
+    ("arm", dict(n_samples=1024, n_horizon=32, cost_terms=("covar", "center", "action"))),   # extended kernel
+]
+
+
+@pytest.mark.parametrize("model,kw", CASES, ids=[f"{m}-{'-'.join(f'{k}{v}' for k, v in kw.items())}" for m, kw in CASES])
+def test_native_dispatch_matches_hip(monkeypatch, model, kw):
+    h, a = _pair(monkeypatch, model, **kw)
+    for e in (h, a):
+        e.run_steps(7)
+    _same(h, a, "7 steps")
+    # a HIP-path control call after the native batch continues its step counter
+    st = _state(model, h.V, shift=0.01)
+    oh, uh, _ = h.step(st)
+    oa, ua, _ = a.step(st)
+    np.testing.assert_array_equal(oa, oh)
+    np.testing.assert_array_equal(ua, uh)
+    # and a native batch after HIP-path steps (device counter re-uploaded), new state
+    for e in (h, a):
+        e.run_steps(5)
+    _same(h, a, "after a control call")
+    h.close()
+    a.close()
+
+
+def test_native_counter_rewind_and_many_batches(monkeypatch):
+    """set_step_counter rewinds the device counter; back-to-back batches without a sync and
+    a batch longer than the queue ring (4096 packets) stay in lock step with HIP."""
+    h, a = _pair(monkeypatch, "arm", n_samples=1024, n_horizon=32)
+    for e in (h, a):
+        e.run_steps(3)
+        e.set_step_counter(5)
+        e.run_steps(4)
+        e.run_steps(2)   # enqueued behind the previous batch (no host sync in between)
+    _same(h, a, "rewind")
+    for e in (h, a):
+        e.run_steps(2500)   # 5000 packets: wraps the 4096-packet ring
+    _same(h, a, "ring wrap")
+    # outputs read straight after a batch (read_outputs waits on the batch's signal)
+    for e in (h, a):
+        e.run_steps(3)
+    oh, _, _ = h.read_outputs()
+    oa, _, _ = a.read_outputs()
+    np.testing.assert_array_equal(oa, oh)
+    h.close()
+    a.close()
+
+
+def test_native_is_the_default(monkeypatch):
+    """auto mode (no MPPI_DISPATCH) dispatches natively on the GPU box; a sharded engine and
+    timing mode say why they stay on HIP."""
+    monkeypatch.delenv("MPPI_DISPATCH", raising=False)
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    e = Engine(make_config("arm", device=0, n_samples=1024, n_horizon=32))
+    e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+    e.set_state(_state("arm"))
+    e.run_steps(3)
+    e.synchronize()
+    assert e.dispatch_info() == "aql"
+    e.enable_timing(True)
+    e.run_steps(2)
+    e.synchronize()
+    assert e.dispatch_info().startswith("hip: per-launch timing"), e.dispatch_info()
+    e.close()
