@@ -317,6 +317,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
     prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
     bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
+    dispatch = eng.dispatch_info()        # "aql" (native packets) or "hip: <why not>"
     bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
     if tim is not None and dist is not None:   # the slowest rank's kernels
         tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
@@ -335,7 +336,8 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.native else None
-    res = {"batches_s": bt, "enqueue_s": benq, "dt": float(np.median(bt)), "tim": tim, "lat": lat, "K": eng.K, "H": eng.H,
+    res = {"batches_s": bt, "enqueue_s": benq, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
+           "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
            "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native,
            "native_error": se.native_error, "world": world,
@@ -429,6 +431,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
                    "enqueue_ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r.get("enqueue_s", [])],
+                   "dispatch": r.get("dispatch"),
                    "basis": "median over the batches; each batch = `warmup` untimed steps, then exactly `steps` "
                             "control steps bracketed by barrier + synchronize (wall clock), max over ranks"},
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,

@@ -22,6 +22,7 @@
 #include <hsa/hsa_ext_amd.h>
 #include <immintrin.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -250,7 +251,7 @@ static bool same_launch(const mppi::LaunchDesc& a, const mppi::LaunchDesc& b, ui
     if (strcmp(a.symbol, b.symbol) != 0 || memcmp(a.grid, b.grid, sizeof a.grid) != 0 ||
         memcmp(a.block, b.block, sizeof a.block) != 0 || a.lds != b.lds || a.arg_bytes != b.arg_bytes)
         return false;
-    if (skip_off + 4 > a.arg_bytes) return memcmp(a.args, b.args, a.arg_bytes) == 0;
+    if (skip_off >= a.arg_bytes || a.arg_bytes - skip_off < 4) return memcmp(a.args, b.args, a.arg_bytes) == 0;
     return memcmp(a.args, b.args, skip_off) == 0 &&
            memcmp(a.args + skip_off + 4, b.args + skip_off + 4, a.arg_bytes - skip_off - 4) == 0;
 }
@@ -263,6 +264,16 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
     if (s->valid && s->step_word == word && s->step_off == step_off && same_launch(roll, s->roll, step_off) &&
         same_launch(fin, s->fin, ~0u))
         return 0;
+    if (getenv("MPPI_AQL_PROFILE") && s->valid) {   // diagnostics: why the blocks are re-uploaded
+        int first = -1;
+        for (uint32_t i = 0; i < roll.arg_bytes && i < s->roll.arg_bytes; ++i)
+            if ((i < step_off || i >= step_off + 4) && roll.args[i] != s->roll.args[i]) { first = (int)i; break; }
+        int ffirst = -1;
+        for (uint32_t i = 0; i < fin.arg_bytes && i < s->fin.arg_bytes; ++i)
+            if (fin.args[i] != s->fin.args[i]) { ffirst = (int)i; break; }
+        fprintf(stderr, "[mppi aql] re-upload: word %u vs %u, rollout args differ at %d, finalize at %d, sym %d/%d\n", word,
+                s->step_word, first, ffirst, strcmp(roll.symbol, s->roll.symbol), strcmp(fin.symbol, s->fin.symbol));
+    }
     Kern kr, kf;
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -293,8 +304,18 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 
 // One kernel-dispatch packet: body first, then header + setup in one release store (the
 // packet processor may read the slot as soon as the header says KERNEL_DISPATCH).
+// diagnostics (tools/): MPPI_AQL_FENCES = "<rollout acquire><rollout release><finalize acquire><finalize
+// release>" scope digits (0 none, 1 agent, 2 system) for the packets before a batch's last; default 1111
+static int g_fence[4] = {-1, -1, -1, -1};
+static void load_fences() {
+    if (g_fence[0] >= 0) return;
+    const char* f = getenv("MPPI_AQL_FENCES");
+    for (int i = 0; i < 4; ++i) g_fence[i] = (f && strlen(f) == 4 && f[i] >= '0' && f[i] <= '2') ? f[i] - '0' : 1;
+}
+static const int kScope[3] = {HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_SYSTEM};
+
 static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l, void* args, hsa_signal_t sig,
-                       bool system_release) {
+                       int acquire, int release) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
     while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
     auto* p = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & (q->size - 1));
@@ -315,9 +336,8 @@ static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l,
     // acquire); the batch's last one releases to system scope (the outputs in host memory)
     const uint16_t header =
         (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
-                   (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                   ((system_release ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT)
-                    << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+                   (kScope[acquire] << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                   (kScope[release] << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint32_t setup = 3u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n((uint32_t*)p, (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
 }
@@ -331,10 +351,11 @@ int step_dispatch(Step* s, int n, std::string* err) {
     const hsa_signal_t none{0};
     void* ra = s->d_args;
     void* fa = s->d_args + kArgSlot;
+    load_fences();
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
-        put(s->q, s->kr, s->roll, ra, none, false);
-        put(s->q, s->kf, s->fin, fa, last ? s->done : none, last);
+        put(s->q, s->kr, s->roll, ra, none, g_fence[0], g_fence[1]);
+        put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
         // the doorbell takes the index of the last packet written
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     }

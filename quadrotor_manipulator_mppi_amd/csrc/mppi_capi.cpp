@@ -1472,11 +1472,17 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
             return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
         }
     }
+    static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: host phase times
+    static double pt[4] = {0, 0, 0, 0};
+    static long pn = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto c0 = now();
     // HIP work still queued on the engine's stream (uploads, an earlier HIP-path step) first
     const hipError_t q = hipStreamQuery(e->stream);
     if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(e->stream));
     else if (q != hipSuccess) return fail(MPPI_ERR_HIP, "engine stream: %s", hipGetErrorString(q));
     // the two launches exactly as the HIP path makes them, described instead of launched
+    const auto c1 = now();
     static thread_local LaunchDesc roll, fin;
     DevParams p = e->dp;
     p.noise_in = nullptr;
@@ -1496,7 +1502,9 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     mppi_aql::set_capture(nullptr);
     if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
     std::string err;
+    const auto c2 = now();
     const int pr = mppi_aql::step_prepare(e->aql, roll, fin, e->step_ctr, kRollStepOff, &err);
+    const auto c3 = now();
     if (pr == -2) {   // not dispatchable natively (a kernel the code objects lack, hidden arguments)
         e->aql_off = true;
         e->aql_why = err;
@@ -1504,6 +1512,14 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     }
     if (pr != 0 || mppi_aql::step_dispatch(e->aql, n, &err) != 0)
         return fail(MPPI_ERR_HIP, "native dispatch: %s", err.c_str());
+    if (prof) {
+        const auto c4 = now();
+        const std::chrono::steady_clock::time_point cs[5] = {c0, c1, c2, c3, c4};
+        for (int i = 0; i < 4; ++i) pt[i] += std::chrono::duration<double, std::micro>(cs[i + 1] - cs[i]).count();
+        if (++pn % 200 == 0)
+            fprintf(stderr, "[mppi aql] per batch (us): stream query %.2f  capture %.2f  prepare %.2f  packets %.2f\n",
+                    pt[0] / pn, pt[1] / pn, pt[2] / pn, pt[3] / pn);
+    }
     e->step_ctr += (uint32_t)n;
     e->out_pending = true;
     e->aql_out = true;
