@@ -30,7 +30,9 @@ MPPI_DIST_BACKEND=gloo MPPI_NATIVE_COMM=0 timeout -k 10 300 python -m torch.dist
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 \
     --latency-steps 20 > $out/bench_gloo2.json 2> $out/bench_gloo2.err
 rc=$?; echo "gloo rehearsal rc=$rc"; [ $rc -eq 0 ] || { tail -30 $out/bench_gloo2.err; exit $rc; }
-bash scripts/gpu_timeline.sh $tag quadrotor_manipulator_mppi_amd/lib/ab/timeline.so arm_c3 wholebody_c4 c4_shard_native1 c4 \
-    > $out/timeline.txt 2>&1
-rc=$?; echo "timeline rc=$rc"
+if [ -f quadrotor_manipulator_mppi_amd/lib/ab/timeline.so ]; then   # (built by scripts/gpu_timeline.sh's recipe)
+  bash scripts/gpu_timeline.sh $tag quadrotor_manipulator_mppi_amd/lib/ab/timeline.so arm_c3 wholebody_c4 c4_shard_native1 c4 \
+      > $out/timeline.txt 2>&1
+  rc=$?; echo "timeline rc=$rc"
+fi
 exit $rc
