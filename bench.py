@@ -317,7 +317,6 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
     prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
     bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
-    dispatch = eng.dispatch_info()        # "aql" (native packets) or "hip: <why not>"
     bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
     if tim is not None and dist is not None:   # the slowest rank's kernels
         tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
@@ -332,6 +331,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     eng.synchronize()
     if not lat:
         se.step(state)
+    dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
     out, u0, st = eng.read_outputs()
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"

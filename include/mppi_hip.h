@@ -264,7 +264,10 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
  * device memory (MPPI_DISPATCH = auto (default) | aql (required) | hip). */
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 
-/* How the last mppi_run_steps was dispatched: "aql", or "hip: <why not native>". */
+/* How the last mppi_run_steps and the last mppi_step were dispatched:
+ * "<aql | hip: why not native>; calls: <aql | hip>".  One-vehicle control calls with device
+ * noise also go out as native packets: the state rides in the rollout's arguments, written
+ * into pinned host memory per call. */
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len);
 
 mppi_status mppi_synchronize(mppi_engine* e);

@@ -48,7 +48,49 @@ struct Device {
     hsa_agent_t agent{};
     std::vector<hsa_executable_t> exes;
     std::unordered_map<std::string, Kern> syms;
+    // device memory the host can write (large BAR): the control calls' argument blocks
+    bool vis_pool_ok = false;
+    hsa_amd_memory_pool_t vis_pool{};
+    hsa_agent_t cpu{};
+    std::string vis_pool_kind;
+    hsa_amd_hdp_flush_t hdp{};
 };
+
+hsa_status_t first_cpu(hsa_agent_t a, void* data) {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+        *(hsa_agent_t*)data = a;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+struct PoolPick {
+    hsa_agent_t cpu;
+    int best_rank;   // 3 kernarg-init, 2 fine-grained, 1 coarse-grained (CPU-accessible in every case)
+    hsa_amd_memory_pool_t pool;
+};
+hsa_status_t pick_pool(hsa_amd_memory_pool_t pool, void* data) {
+    auto* pk = (PoolPick*)data;
+    hsa_amd_segment_t seg;
+    uint32_t flags = 0;
+    bool alloc = false;
+    hsa_amd_memory_pool_access_t acc = HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED;
+    if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+        seg != HSA_AMD_SEGMENT_GLOBAL)
+        return HSA_STATUS_SUCCESS;
+    if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS ||
+        hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc) != HSA_STATUS_SUCCESS ||
+        !alloc)
+        return HSA_STATUS_SUCCESS;
+    if (hsa_amd_agent_memory_pool_get_info(pk->cpu, pool, HSA_AMD_AGENT_MEMORY_POOL_INFO_ACCESS, &acc) !=
+            HSA_STATUS_SUCCESS || acc == HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED)
+        return HSA_STATUS_SUCCESS;
+    const int rank = (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) ? 3
+                     : (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) ? 2 : 1;
+    if (rank > pk->best_rank) { pk->best_rank = rank; pk->pool = pool; }
+    return HSA_STATUS_SUCCESS;
+}
 std::mutex g_mu;
 std::map<int, Device> g_dev;
 
@@ -140,6 +182,22 @@ Device* device_for(int ordinal) {
         }
         d.exes.push_back(ex);
     }
+    // a GPU memory pool the host can write directly (large BAR), for the control calls'
+    // rollout arguments; without one they go to pinned host memory
+    hsa_agent_t cpu{};
+    if (hsa_iterate_agents(first_cpu, &cpu) == HSA_STATUS_INFO_BREAK && !getenv("MPPI_AQL_CALL_HOSTMEM")) {
+        PoolPick pk{cpu, 0, {}};
+        hsa_amd_agent_iterate_memory_pools(d.agent, pick_pool, &pk);
+        if (pk.best_rank > 0 &&
+            hsa_agent_get_info(d.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &d.hdp) == HSA_STATUS_SUCCESS &&
+            d.hdp.HDP_MEM_FLUSH_CNTL) {
+            d.vis_pool_ok = true;
+            d.vis_pool = pk.pool;
+            d.cpu = cpu;
+            d.vis_pool_kind = pk.best_rank == 3 ? "device kernarg pool" : pk.best_rank == 2 ? "device fine-grained"
+                                                                                             : "device coarse-grained";
+        }
+    }
     d.ok = true;
     return &d;
 }
@@ -173,14 +231,29 @@ extern "C" mppi::LaunchDesc* mppi_capture_target(void) { return t_capture; }
 namespace mppi_aql {
 
 constexpr uint32_t kQueueSize = 4096;   // packets (256 KB ring)
-constexpr size_t kArgSlot = 4096;       // bytes per argument block: [rollout | finalize]
+constexpr size_t kArgSlot = 4096;       // bytes per argument block: [rollout | finalize | call finalize]
+// control calls rotate through this many rollout argument blocks (each call a fresh address,
+// as HIP's own kernel-argument ring: no copy of an earlier call's block can sit in a cache)
+constexpr uint32_t kCallSlots = 16;
+// the batch path's (rollout, finalize) argument pair: re-uploads rotate over this many pairs
+constexpr uint32_t kBatchSlots = 4;
 
 struct Step {
     Device* dev = nullptr;
     hsa_queue_t* q = nullptr;
     hsa_signal_t done{0};                 // outstanding batches; each batch's last packet decrements it
     std::atomic<int> qerr{0};             // HSA status of an asynchronous queue error
-    unsigned char* d_args = nullptr;      // device: rollout arguments at 0, finalize at kArgSlot
+    unsigned char* d_args = nullptr;      // device: the control call's finalize at 0, then kBatchSlots
+                                          // (rollout, finalize) pairs for batches
+    uint32_t batch_slot = 0;              // the pair the batches use now
+    unsigned char* h_call = nullptr;      // the control calls' rollout arguments: kCallSlots blocks in
+    unsigned char* h_call_dev = nullptr;  //   host-writable device memory (else pinned host memory),
+    bool call_vis = false;                //   host and device addresses; call_vis = device memory
+    uint32_t call_slot = 0;
+    mppi::LaunchDesc fin_call{};          // what the call's finalize block holds
+    Kern kc_r, kc_f;
+    bool call_valid = false;
+    bool call_unread = false;             // the last call's outputs not yet seen (step_call_read)
     mppi::LaunchDesc roll{}, fin{};       // what the device blocks hold (step word as uploaded)
     Kern kr, kf;
     uint32_t step_off = 0, step_word = 0; // the resident rollout's dispatch-id relative step word
@@ -209,8 +282,24 @@ Step* step_create(int device, std::string* why) {
         delete s;
         return nullptr;
     }
-    if (hipMalloc(&s->d_args, 2 * kArgSlot) != hipSuccess) {
-        *why = "hipMalloc of the argument blocks failed";
+    if (d->vis_pool_ok) {   // host-writable device memory for the calls' argument blocks
+        void* p = nullptr;
+        if (hsa_amd_memory_pool_allocate(d->vis_pool, kCallSlots * kArgSlot, 0, &p) == HSA_STATUS_SUCCESS) {
+            if (hsa_amd_agents_allow_access(1, &d->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
+                s->h_call = s->h_call_dev = (unsigned char*)p;
+                s->call_vis = true;
+            } else {
+                hsa_amd_memory_pool_free(p);
+            }
+        }
+    }
+    if (hipMalloc(&s->d_args, (1 + 2 * kBatchSlots) * kArgSlot) != hipSuccess ||
+        (!s->call_vis &&
+         (hipHostMalloc((void**)&s->h_call, kCallSlots * kArgSlot, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&s->h_call_dev, s->h_call, 0) != hipSuccess))) {
+        *why = "allocating the argument blocks failed";
+        if (s->d_args) (void)hipFree(s->d_args);
+        if (s->h_call) { if (s->call_vis) hsa_amd_memory_pool_free(s->h_call); else (void)hipHostFree(s->h_call); }
         hsa_signal_destroy(s->done);
         hsa_queue_destroy(s->q);
         delete s;
@@ -226,6 +315,7 @@ void step_destroy(Step* s) {
     hsa_signal_destroy(s->done);
     hsa_queue_destroy(s->q);
     (void)hipFree(s->d_args);
+    if (s->call_vis) hsa_amd_memory_pool_free(s->h_call); else (void)hipHostFree(s->h_call);
     delete s;
 }
 
@@ -255,6 +345,8 @@ static bool same_launch(const mppi::LaunchDesc& a, const mppi::LaunchDesc& b, ui
     return memcmp(a.args, b.args, skip_off) == 0 &&
            memcmp(a.args + skip_off + 4, b.args + skip_off + 4, a.arg_bytes - skip_off - 4) == 0;
 }
+
+static unsigned char* batch_args(Step* s) { return s->d_args + (1 + 2 * (size_t)s->batch_slot) * kArgSlot; }
 
 int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
                  uint32_t step_off, std::string* err) {
@@ -287,7 +379,9 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
     memcpy(h.data(), roll.args, roll.arg_bytes);
     memcpy(h.data() + step_off, &word, 4);
     memcpy(h.data() + kArgSlot, fin.args, fin.arg_bytes);
-    if (hipMemcpy(s->d_args, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    // a fresh pair of blocks for every upload (no cached copy of an earlier upload can be read)
+    s->batch_slot = (s->batch_slot + 1) % kBatchSlots;
+    if (hipMemcpy(batch_args(s), h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
         *err = "uploading the argument blocks failed";
         s->valid = false;
         return -1;
@@ -349,8 +443,8 @@ int step_dispatch(Step* s, int n, std::string* err) {
     hsa_signal_add_relaxed(s->done, 1);   // this batch's completion
     ++s->outstanding;
     const hsa_signal_t none{0};
-    void* ra = s->d_args;
-    void* fa = s->d_args + kArgSlot;
+    void* ra = batch_args(s);
+    void* fa = batch_args(s) + kArgSlot;
     load_fences();
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
@@ -360,6 +454,76 @@ int step_dispatch(Step* s, int n, std::string* err) {
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     }
     return 0;
+}
+
+int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
+              uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err) {
+    if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
+    Kern kr, kf;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
+    }
+    if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
+    if (step_off + 4 > roll.arg_bytes || seq_off + 4 > roll.arg_bytes) { *err = "call words outside the arguments"; return -2; }
+    // the host block is rewritten below: the previous call's rollout must have read it.  The
+    // engine reads every call's outputs before the next call (its flag: that rollout has run),
+    // so only an unread call waits; a queued batch does not read this block.
+    if (s->call_unread && s->outstanding && step_wait(s, 60000, err) != 0) return -1;
+    if (!s->call_valid || !same_launch(fin, s->fin_call, ~0u)) {
+        if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
+        std::vector<unsigned char> h(kArgSlot, 0);
+        memcpy(h.data(), fin.args, fin.arg_bytes);
+        if (hipMemcpy(s->d_args, h.data(), kArgSlot, hipMemcpyHostToDevice) != hipSuccess) {
+            *err = "uploading the call's finalize arguments failed";
+            s->call_valid = false;
+            return -1;
+        }
+        s->fin_call = fin;
+        s->call_valid = true;
+    }
+    s->kc_r = kr;
+    s->kc_f = kf;
+    const uint64_t r = hsa_queue_load_write_index_relaxed(s->q);   // this call's rollout packet
+    const uint32_t word = step - (uint32_t)(r >> 1);
+    *seq = 0x80000000u | (uint32_t)(r >> 1);
+    const uint32_t slot = s->call_slot++ % kCallSlots;
+    unsigned char* blk = s->h_call + (size_t)slot * kArgSlot;
+    alignas(16) unsigned char tmp[kArgSlot];
+    memcpy(tmp, roll.args, roll.arg_bytes);
+    memcpy(tmp + step_off, &word, 4);
+    memcpy(tmp + seq_off, seq, 4);
+    const uint32_t nb = (roll.arg_bytes + 63) & ~63u;   // whole 64 B lines
+    memset(tmp + roll.arg_bytes, 0, nb - roll.arg_bytes);
+    memcpy(blk, tmp, nb);
+    if (s->call_vis) {
+        // device memory written through the BAR: drain the write-combining buffers, flush the
+        // host data path and read the flush register back (the writes have landed) before the
+        // packet can send the command processor to the block
+        _mm_sfence();
+        volatile uint32_t* f = s->dev->hdp.HDP_MEM_FLUSH_CNTL;
+        *f = 1u;
+        (void)*f;
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    hsa_signal_add_relaxed(s->done, 1);
+    ++s->outstanding;
+    s->call_unread = true;
+    const hsa_signal_t none{0};
+    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, 1, 1);
+    put(s->q, kf, fin, s->d_args, s->done, 1, 2);
+    hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
+    return 0;
+}
+
+int step_error(Step* s) { return s ? s->qerr.load() : 0; }
+
+const char* step_call_memory(Step* s) {
+    return !s ? "" : s->call_vis ? s->dev->vis_pool_kind.c_str() : "pinned host memory";
+}
+
+void step_call_read(Step* s) {
+    if (s) s->call_unread = false;
 }
 
 int step_wait(Step* s, int timeout_ms, std::string* err) {
@@ -378,6 +542,7 @@ int step_wait(Step* s, int timeout_ms, std::string* err) {
         _mm_pause();
     }
     s->outstanding = 0;
+    s->call_unread = false;
     return 0;
 }
 

@@ -35,6 +35,22 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 // n (rollout, finalize) pairs, each kernel dependent on the one before; the last finalize
 // carries the completion signal and a system-scope release.
 int step_dispatch(Step* s, int n, std::string* err);
+// One control call: a (rollout, finalize) pair whose rollout arguments (the state changes every
+// call) are written by the host into a fresh block of a small ring in host-writable device
+// memory (pinned host memory without one), the finalize's from a static device block.  The host
+// writes `seq` into the rollout's arguments at seq_off (the vehicle constants' spare word,
+// which the rollout hands to the finalize) and polls the completion flags for it: bit 31 set,
+// unique per call.  0 / -2 / -1 as step_prepare.
+int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
+              uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err);
+// The last call's outputs have been seen (its completion flags): its rollout has run.
+void step_call_read(Step* s);
+// Where the control calls' rollout arguments live ("device kernarg pool", "device
+// fine-grained", "device coarse-grained": written by the host through the BAR; or "pinned host
+// memory", read over PCIe by every block: MPPI_AQL_CALL_HOSTMEM=1 or no host-writable pool).
+const char* step_call_memory(Step* s);
+// The queue's asynchronous error, if any (0 = none).
+int step_error(Step* s);
 // Until every dispatched pair has completed.  -1 on a queue error or after timeout_ms.
 int step_wait(Step* s, int timeout_ms, std::string* err);
 bool step_busy(Step* s);

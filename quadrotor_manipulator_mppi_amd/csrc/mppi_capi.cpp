@@ -373,6 +373,8 @@ struct mppi_engine {
     bool aql_off = false;               // this engine's launches are not dispatchable natively
     std::string aql_why = "no mppi_run_steps yet";   // why the last run went through HIP ("" = native)
     bool aql_out = false;               // the pending outputs come from a native batch
+    bool aql_call = false;              // ... from a native control call (flags carry bit 31)
+    bool calls_native = false;          // the last mppi_step went out as native packets
 };
 
 namespace {
@@ -1300,8 +1302,8 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     if (record_out && !e->no_flag_dbg) {   // a fresh value per read step, never 0 (the flags start zeroed):
                                            // the flags the previous read step left can never satisfy this
                                            // step's wait
-        f.seq = ++e->seq_ctr;
-        if (f.seq == 0u) f.seq = ++e->seq_ctr;
+        f.seq = ++e->seq_ctr & 0x7FFFFFFFu;   // (bit 31: native control calls' numbers)
+        if (f.seq == 0u) f.seq = ++e->seq_ctr & 0x7FFFFFFFu;
     }
     final_records(e, f);
     if (e->out_dbg == 1 && !record_out) f.tail = e->d_tail + kTailScratch;   // diagnostic (MPPI_DEBUG_OUT)
@@ -1315,6 +1317,7 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
     ++e->step_ctr;
     e->out_pending = record_out;
     e->aql_out = false;
+    e->aql_call = false;
     return MPPI_OK;
 }
 
@@ -1331,6 +1334,26 @@ mppi_status mppi_finalize(mppi_engine* e) {
 // hundred polls, which also surfaces a faulted queue as an error.
 static mppi_status wait_outputs(mppi_engine* e) {
     if (e->aql_out) return aql_join(e);   // a native batch: its completion signal (system-scope release)
+    if (e->aql_call) {   // a native control call: its flags, the queue's error state as the backstop
+        const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
+        const int n = e->V * e->A;
+        const uint32_t want = e->out_seq;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t it = 1;; ++it) {
+            int j = 0;
+            while (j < n && fl[j] == want) ++j;
+            if (j == n) break;
+            if ((it & 255u) == 0) {
+                if (const int q = mppi_aql::step_error(e->aql)) return fail(MPPI_ERR_HIP, "native queue error %d", q);
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                    return fail(MPPI_ERR_HIP, "native control call: no outputs after 60 s");
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        mppi_aql::step_call_read(e->aql);
+        return MPPI_OK;
+    }
     if (!e->event_wait) {
         const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
         const int n = e->V * e->A;
@@ -1357,7 +1380,8 @@ static mppi_status wait_outputs(mppi_engine* e) {
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (!e->out_pending) return fail(MPPI_ERR_STATE, "no finalised step to read");
-    if (use_device(e)) return MPPI_ERR_HIP;
+    if (e->aql_call) HIP_TRY(hipSetDevice(e->cfg.device));   // (its flags, not the queue's drain)
+    else if (use_device(e)) return MPPI_ERR_HIP;
     {   mppi_status st = wait_outputs(e);
         if (st != MPPI_OK) return st; }
     if (e->d_stamps) {   // diagnostic: average phase cycles over all waves
@@ -1415,12 +1439,21 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
     return MPPI_OK;
 }
 
+static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* used);
+
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out, float* u0,
                       mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (sharded(e) && !e->comm)
         return fail(MPPI_ERR_STATE, "mppi_step on a shard needs mppi_comm_init (or use the split phases)");
     mppi_status st;
+    if (e->cfg.noise_mode == MPPI_NOISE_PHILOX && e->V == 1 && !sharded(e)) {   // one vehicle: native packets
+        bool used = false;
+        if ((st = control_call_aql(e, state, &used)) != MPPI_OK) return st;
+        e->calls_native = used;
+        if (used) return mppi_read_outputs(e, out, u0, stats);
+    }
+    e->calls_native = false;
     if (state && (st = mppi_set_state(e, state)) != MPPI_OK) return st;
     const float* dn = nullptr;
     if (e->cfg.noise_mode == MPPI_NOISE_INJECTED) {
@@ -1455,23 +1488,25 @@ constexpr int32_t kNoiseStepFromId = 0x100;   // = mppi_device.h
 
 // n steps as native AQL packets (mppi_aql.cpp).  *used = false: the caller runs them through
 // HIP (auto mode, native dispatch unavailable for this engine; e->aql_why says why).
+// the engine's native queue, created on first use; false when native dispatch is off for it
+static bool aql_ready(mppi_engine* e) {
+    if (e->aql_off) return false;
+    if (!e->aql && !e->aql_tried) {
+        e->aql_tried = true;
+        std::string why;
+        if (hipSetDevice(e->cfg.device) == hipSuccess) e->aql = mppi_aql::step_create(e->cfg.device, &why);
+        else why = "hipSetDevice failed";
+        if (!e->aql) e->aql_why = why;
+    }
+    if (!e->aql) e->aql_off = true;
+    return e->aql != nullptr;
+}
+
 static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     *used = false;
     if (const char* why = aql_ineligible(e)) { e->aql_why = why; return MPPI_OK; }
-    if (e->aql_off) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
+    if (!aql_ready(e)) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
     HIP_TRY(hipSetDevice(e->cfg.device));
-    if (!e->aql) {
-        if (!e->aql_tried) {
-            e->aql_tried = true;
-            std::string why;
-            e->aql = mppi_aql::step_create(e->cfg.device, &why);
-            if (!e->aql) e->aql_why = why;
-        }
-        if (!e->aql) {
-            e->aql_off = true;
-            return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
-        }
-    }
     static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: host phase times
     static double pt[4] = {0, 0, 0, 0};
     static long pn = 0;
@@ -1523,7 +1558,69 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     e->step_ctr += (uint32_t)n;
     e->out_pending = true;
     e->aql_out = true;
+    e->aql_call = false;
     e->aql_why.clear();
+    *used = true;
+    return MPPI_OK;
+}
+
+// One control call (V == 1) as a native (rollout, finalize) pair: the state goes into the
+// rollout's arguments in pinned host memory (its vehicle constants), the finalize's arguments
+// stay resident, and the call's completion flags carry a bit-31 sequence number the host
+// wrote next to the constants (mppi_aql.h step_call).  *used = false: the HIP path runs it.
+static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* used) {
+    *used = false;
+    if (aql_ineligible(e) || e->event_wait) return MPPI_OK;
+    if (!aql_ready(e)) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str())
+                                               : MPPI_OK;
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    if (state) {   // mppi_set_state's work for one vehicle: host-side constants only
+        std::memcpy(e->state.data(), state, sizeof(double) * e->state.size());
+        e->state_set = true;
+        mppi_status st = build_vehicle_consts(e);
+        if (st != MPPI_OK) return st;
+    }
+    if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_step before mppi_set_state");
+    {   // HIP work queued on the engine's stream first (0.1 us when there is none)
+        const hipError_t q = hipStreamQuery(e->stream);
+        if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(e->stream));
+        else if (q != hipSuccess) return fail(MPPI_ERR_HIP, "engine stream: %s", hipGetErrorString(q));
+    }
+    static thread_local LaunchDesc roll, fin;
+    DevParams p = e->dp;
+    p.noise_in = nullptr;
+    p.vc0 = e->h_vc[0];
+    p.step_ctr = 0u;
+    p.noise_mode |= kNoiseStepFromId;
+    FinParams f = e->fp;
+    f.mode = 0;
+    f.seq = kSeqFromVc;
+    final_records(e, f);
+    mppi_aql::set_capture(&roll);
+    int rc = mppi_launch_rollout(&p, e->threads, e->stream);
+    if (rc == 0) {
+        mppi_aql::set_capture(&fin);
+        rc = mppi_launch_finalize(&f, e->stream);
+    }
+    mppi_aql::set_capture(nullptr);
+    if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
+    // the vehicle constants' spare word inside the rollout's last argument (DevParams by value)
+    const uint32_t seq_off = roll.arg_bytes - (uint32_t)sizeof(DevParams) + (uint32_t)offsetof(DevParams, vc0) +
+                             (uint32_t)offsetof(VehicleConst, _pad);
+    std::string err;
+    uint32_t seq = 0;
+    const int pr = mppi_aql::step_call(e->aql, roll, fin, e->step_ctr, kRollStepOff, seq_off, &seq, &err);
+    if (pr == -2) {
+        e->aql_off = true;
+        e->aql_why = err;
+        return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", err.c_str()) : MPPI_OK;
+    }
+    if (pr != 0) return fail(MPPI_ERR_HIP, "native dispatch: %s", err.c_str());
+    ++e->step_ctr;
+    e->out_seq = seq;
+    e->out_pending = true;
+    e->aql_out = false;
+    e->aql_call = true;
     *used = true;
     return MPPI_OK;
 }
@@ -1683,7 +1780,9 @@ mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us
 
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len) {
     if (!e || !buf || len <= 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_dispatch_info: bad arguments");
-    snprintf(buf, (size_t)len, "%s%s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str());
+    snprintf(buf, (size_t)len, "%s%s; calls: %s%s%s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str(),
+             e->calls_native ? "aql (arguments in " : "hip", e->calls_native ? mppi_aql::step_call_memory(e->aql) : "",
+             e->calls_native ? ")" : "");
     return MPPI_OK;
 }
 

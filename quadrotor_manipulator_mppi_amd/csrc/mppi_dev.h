@@ -37,7 +37,7 @@ struct VehicleConst {
                           //      fixed joints; column 3 = R * (their translation), p(k,t) is added
     float tpos[3];        // target position
     float tR[9];          // target rotation (quaternion_to_matrix, xyzw)
-    float _pad[4];
+    float _pad[4];        // [0]: a native control call's sequence number (bits; k_finalize, kSeqFromVc)
     float qc[kMaxJ];      // extra cost terms (mppi_config): centering target and joint limits
     float qlo[kMaxJ];     //   per arm joint (the same for every vehicle)
     float qhi[kMaxJ];     // sizeof = 688 (16-byte multiple: keeps the dynamic LDS base aligned)
@@ -141,6 +141,10 @@ struct FinTail {
     float sg[kMaxW];
 };
 enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailSlots = 3 };
+// k_finalize's sequence argument: this value = take the step's sequence number from the vehicle
+// constants (VehicleConst::_pad[0]; native control calls, mppi_aql.cpp).  HIP-path sequence
+// numbers stay below 2^31, native ones have bit 31 set: the two never meet in the flags.
+constexpr uint32_t kSeqFromVc = 0xFFFFFFFFu;
 
 // A kernel launch as data (mppi_aql.cpp): while a LaunchDesc is installed for the calling
 // thread (mppi_capture_target), the launchers fill it in instead of launching through HIP --

@@ -136,6 +136,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     float coef = 0.0f, dt = 0.0f, dt2 = 0.0f;
     int32_t mode = 0, model = 0, qoff = 0, nq = 0, sf64 = 0, odim = 0;
     const uint32_t seq = seq_arg;
+    // native control calls (mppi_aql.cpp): the step's sequence number travels with the vehicle
+    // constants (VehicleConst::_pad[0], written by the host into the rollout's arguments, handed
+    // over by the rollout's block 0), so the finalize's own argument block stays static
+    uint32_t seqv = seq;
     float *wraw = nullptr, *wsmooth = nullptr, *u0p = nullptr, *stats = nullptr;
     double* outp = nullptr;
     uint32_t* flags = nullptr;
@@ -170,6 +174,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             const VehicleConst* vcp = vcb + v;
             x0f = *(gfloat*)(vcp->pos0f + a); v0f = *(gfloat*)(vcp->vel0f + a);
             x0d = *(gdouble*)(vcp->pos0 + a); v0d = *(gdouble*)(vcp->vel0 + a);
+            if (seq == kSeqFromVc) seqv = *(const __attribute__((address_space(1))) uint32_t*)(vcp->_pad);
         }
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
@@ -377,9 +382,9 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // acknowledgment let 3 of 9000 calls read outputs their flag did not cover, and
         // system-scope output stores (written through, acknowledged from the host) plus that
         // wait were correct but 2 us slower per control call.
-        if (seq != 0u) {
+        if (seqv != 0u) {
             __threadfence_system();
-            __hip_atomic_store(flags + (size_t)v * A + a, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(flags + (size_t)v * A + a, seqv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     FSTAMP(6);

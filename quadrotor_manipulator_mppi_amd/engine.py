@@ -279,7 +279,7 @@ class Engine:
         capi.check(self._L.mppi_synchronize(self._h), "synchronize")
 
     def dispatch_info(self) -> str:
-        """How the last run_steps was dispatched: "aql" (native packets) or "hip: <why>"."""
+        """How the last run_steps / step were dispatched: "<aql | hip: why>; calls: <aql | hip>"."""
         buf = C.create_string_buffer(256)
         capi.check(self._L.mppi_dispatch_info(self._h, buf, len(buf)), "dispatch_info")
         return buf.value.decode(errors="replace")

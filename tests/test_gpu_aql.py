@@ -1,9 +1,9 @@
-"""Native dispatch (csrc/mppi_aql.cpp): mppi_run_steps as raw AQL packets on the engine's own
-HSA queue must compute exactly what the HIP launches compute -- the same kernels (loaded
-from the library's code objects), the same arguments (captured from the launchers), the
-Philox step counter advanced on the device by the finalize.  Every case runs one engine per
-dispatch mode on identical inputs and compares bit for bit: u_prev, the outputs, the costs,
-and the step after (a HIP-path control call must continue the native counter)."""
+"""Native dispatch (csrc/mppi_aql.cpp): mppi_run_steps and one-vehicle mppi_step as raw AQL
+packets on the engine's own HSA queue must compute exactly what the HIP launches compute --
+the same kernels (loaded from the library's code objects), the same arguments (captured from
+the launchers), the Philox step counter taken from the dispatch id.  Every case runs one
+engine per dispatch mode on identical inputs and compares bit for bit: u_prev, the outputs,
+the costs, and the control call after a batch (it must continue the batch's counter)."""
 import numpy as np
 import pytest
 
@@ -46,7 +46,7 @@ def _pair(monkeypatch, model, **kw):
 def _same(h, a, what):
     h.synchronize()
     a.synchronize()
-    assert a.dispatch_info() == "aql", a.dispatch_info()
+    assert a.dispatch_info().startswith("aql;"), a.dispatch_info()
     assert h.dispatch_info().startswith("hip"), h.dispatch_info()
     np.testing.assert_array_equal(a.get_u_prev(), h.get_u_prev(), err_msg=what + ": u_prev")
     np.testing.assert_array_equal(a.get_costs(), h.get_costs(), err_msg=what + ": costs")
@@ -76,13 +76,13 @@ def test_native_dispatch_matches_hip(monkeypatch, model, kw):
     for e in (h, a):
         e.run_steps(7)
     _same(h, a, "7 steps")
-    # a HIP-path control call after the native batch continues its step counter
+    # a control call after the batch (native on the aql engine for one vehicle) continues its counter
     st = _state(model, h.V, shift=0.01)
     oh, uh, _ = h.step(st)
     oa, ua, _ = a.step(st)
     np.testing.assert_array_equal(oa, oh)
     np.testing.assert_array_equal(ua, uh)
-    # and a native batch after HIP-path steps (device counter re-uploaded), new state
+    # and a native batch after the call, at the call's new state (argument block re-uploaded)
     for e in (h, a):
         e.run_steps(5)
     _same(h, a, "after a control call")
@@ -123,9 +123,46 @@ def test_native_is_the_default(monkeypatch):
     e.set_state(_state("arm"))
     e.run_steps(3)
     e.synchronize()
-    assert e.dispatch_info() == "aql"
+    assert e.dispatch_info().startswith("aql;")
     e.enable_timing(True)
     e.run_steps(2)
     e.synchronize()
     assert e.dispatch_info().startswith("hip: per-launch timing"), e.dispatch_info()
     e.close()
+
+
+CALL_CASES = [("arm", dict(n_samples=4096, n_horizon=32)), ("arm", dict(n_samples=1024, n_horizon=32, state_f64=False)),
+              ("drone", dict(n_samples=4096, n_horizon=32)), ("wholebody", dict(n_samples=8192, n_horizon=64)),
+              ("quadrotor", dict(n_samples=1024, n_horizon=32))]
+
+
+@pytest.mark.parametrize("model,kw", CALL_CASES, ids=[f"{m}-{kw['n_samples']}-{kw['n_horizon']}" for m, kw in CALL_CASES])
+def test_native_control_calls_match_hip(monkeypatch, model, kw):
+    """mppi_step as native packets (the state in the rollout's arguments in pinned host memory,
+    completion by the bit-31 flags): every call's outputs, u0 and stats bit-identical to the HIP
+    path's under a changing state, interleaved with native batches; the outputs read behind
+    the flags equal a re-read after a full synchronize."""
+    h, a = _pair(monkeypatch, model, **kw)
+    rng = np.random.default_rng(5)
+    base = _state(model)[0]
+    for i in range(200):
+        st = base.copy()
+        st[:3] += rng.normal(0, 0.05, 3)
+        oh, uh, sh = h.step(st)
+        oa, ua, sa = a.step(st)
+        np.testing.assert_array_equal(oa, oh, err_msg=f"call {i}")
+        np.testing.assert_array_equal(ua, uh, err_msg=f"call {i}")
+        assert sa[0].rho == sh[0].rho and sa[0].eta == sh[0].eta, i
+        if i % 50 == 49:   # a batch between the calls, then a synchronised re-read
+            for e in (h, a):
+                e.run_steps(3)
+            _same(h, a, f"batch after call {i}")
+        elif i % 10 == 3:
+            a.synchronize()
+            oa2, ua2, _ = a.read_outputs()
+            np.testing.assert_array_equal(oa2, oa)
+            np.testing.assert_array_equal(ua2, ua)
+    assert "calls: aql" in a.dispatch_info(), a.dispatch_info()
+    assert h.dispatch_info().endswith("calls: hip"), h.dispatch_info()
+    h.close()
+    a.close()
