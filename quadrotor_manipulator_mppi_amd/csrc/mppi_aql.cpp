@@ -398,13 +398,23 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 
 // One kernel-dispatch packet: body first, then header + setup in one release store (the
 // packet processor may read the slot as soon as the header says KERNEL_DISPATCH).
-// diagnostics (tools/): MPPI_AQL_FENCES = "<rollout acquire><rollout release><finalize acquire><finalize
-// release>" scope digits (0 none, 1 agent, 2 system) for the packets before a batch's last; default 1111
+// Packet fence scopes (0 none, 1 agent, 2 system): rollout acquire, rollout release, finalize
+// acquire, finalize release (a batch's last finalize releases at system scope).  What one
+// kernel of the step reads from the other is written through at device scope and drained
+// before the writing waves end: the rollouts' record bodies, headers and handed-over vehicle
+// constants (mppi_rollout.h drain_stores), the finalize's u_prev.  So neither packet carries
+// a release, whose end-of-kernel L2 writeback cost up to ~0.8 us per C3 step
+// (tools/aql_fence_probe.py).  What stays dirty in the L2s (the costs S, the readback copies
+// of w_eps) is only read after a batch, behind its system-scope release, and every line of it
+// is written by the same block, hence the same XCD, at every step.  Every acquire stays at
+// agent scope (it invalidates the lines an earlier step left in the L2s: the records, u_prev).
+// Diagnostics: MPPI_AQL_FENCES = four digits.
 static int g_fence[4] = {-1, -1, -1, -1};
 static void load_fences() {
     if (g_fence[0] >= 0) return;
     const char* f = getenv("MPPI_AQL_FENCES");
-    for (int i = 0; i < 4; ++i) g_fence[i] = (f && strlen(f) == 4 && f[i] >= '0' && f[i] <= '2') ? f[i] - '0' : 1;
+    const char* def = "1010";
+    for (int i = 0; i < 4; ++i) g_fence[i] = (f && strlen(f) == 4 && f[i] >= '0' && f[i] <= '2') ? f[i] - '0' : def[i] - '0';
 }
 static const int kScope[3] = {HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_SYSTEM};
 
@@ -510,8 +520,9 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     ++s->outstanding;
     s->call_unread = true;
     const hsa_signal_t none{0};
-    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, 1, 1);
-    put(s->q, kf, fin, s->d_args, s->done, 1, 2);
+    load_fences();
+    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, g_fence[0], g_fence[1]);
+    put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
     hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     return 0;
 }

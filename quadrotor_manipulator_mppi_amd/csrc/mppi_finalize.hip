@@ -334,7 +334,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const float un = u_old + sm;
     if (own) {
         if (wsmooth) wsmooth[((size_t)v * H + t) * A + a] = sm;
-        if (!(MPPI_FIN_KO & 32)) up[t * A + a] = un;   // (32: timing knockout, u_prev not written)
+        // written through at device scope (the next rollout reads it on every XCD), drained at
+        // the end: the native dispatch's finalize packets then need no release (mppi_aql.cpp)
+        if (!(MPPI_FIN_KO & 32))   // (32: timing knockout, u_prev not written)
+            __hip_atomic_store(up + t * A + a, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!(MPPI_FIN_KO & 2) && sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
 #pragma clang fp contract(off)
@@ -389,6 +392,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     }
     FSTAMP(6);
     FSTAMPRT(14);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only

@@ -495,6 +495,28 @@ __device__ __forceinline__ void wt_store(float* base_uniform, uint32_t byte_off,
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base_uniform, 0, (int)0xFFFFFFFFu, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)byte_off, 0, MPPI_REC_AUX);
 }
+// the record header (rho, eta, eta2, nan) of one block, written through like the bodies
+__device__ __forceinline__ void wt_store4(float* base_uniform, uint32_t byte_off, float4 x) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base_uniform, 0, (int)0xFFFFFFFFu, 0x00020000);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)byte_off, 0, MPPI_REC_AUX);
+}
+// A pointer the compiler keeps in SGPRs (its halves read from the first lane): built from
+// kernel arguments through 64-bit VALU math it lands in VGPRs, and a buffer resource over it
+// became a waterfall loop around every store.
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+// The rollout's outputs the finalize reads (record bodies and headers, and the vehicle
+// constants block 0 hands over) are written through at device scope; every wave waits for its
+// stores before it ends.  So they are visible device-wide when the kernel completes, and the
+// native dispatch's rollout packet needs no release fence (the end-of-kernel L2 writeback,
+// ~0.8 us per step at C3; mppi_aql.cpp).
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
 // (the DPP wait states of one dim are filled by the others).  Each step is one
@@ -713,12 +735,13 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     }
     if (tid < kVCW) {
         ((int*)&vcv)[tid] = vcr;
-        if (VONE && blockIdx.x == 0) ((int*)pk.vc)[tid] = vcr;   // hand vc0 to the finalize
+        if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize (written through)
+            __hip_atomic_store((int*)pk.vc + tid, vcr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int i = tid + nthr; i < kVCW; i += nthr) {   // nthr < 124
         const int x = VONE ? ((const int*)&pk.vc0)[i] : ((const int*)(pk.vc + v))[i];
         ((int*)&vcv)[i] = x;
-        if (VONE && blockIdx.x == 0) ((int*)pk.vc)[i] = x;
+        if (VONE && blockIdx.x == 0) __hip_atomic_store((int*)pk.vc + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMPW(8);
     if (!(MPPI_KO & 256)) lds_barrier();
@@ -1179,14 +1202,14 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             eta2 += fw[w] * fw[w] * wsh[w * wstride + 2];
             nanf = fmaxf(nanf, wsh[w * wstride + 3]);
         }
-        *reinterpret_cast<float4*>(p.hdr + ((size_t)v * p.nb + blockIdx.x) * 4) = make_float4(rho_b, eta, eta2, nanf);
+        wt_store4(uniform_ptr(p.hdr), ((uint32_t)v * (uint32_t)p.nb + blockIdx.x) * 16u, make_float4(rho_b, eta, eta2, nanf));
     }
     // record body, dim-major: rdata[v][a][block][t] = sum_w f_w sum_segments acc_w[seg*L + t].
     // (a, t) of element i without an integer division (~25 VALU): a = trunc((i + 1/2) / H)
     // in fp32 is exact, the quotient's error (< 1e-5 for i < A*H <= 2560) being far below
     // the 1/(2H) margin; 32-bit record indices (V*A*nb*H < 2^31, checked at create).
-    const float rH = 1.0f / (float)H;
-    float* const rdata_v = p.rdata + (size_t)v * NA * p.nb * H;   // this vehicle's bodies (< 1 GiB)
+    const float rH = __builtin_amdgcn_rcpf((float)H);   // (1 ulp: far inside the 1/(2H) margin)
+    float* const rdata_v = uniform_ptr(p.rdata + (size_t)v * NA * p.nb * H);   // this vehicle's bodies (< 1 GiB)
     const uint32_t rbase = blockIdx.x * (uint32_t)H;
     const uint32_t rstride = (uint32_t)p.nb * (uint32_t)H;
     for (int i = tid; i < ((MPPI_KO & 64) ? 0 : HA); i += nthr) {
@@ -1204,6 +1227,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     }
     STAMP(7);
     STAMPRT(14);
+    drain_stores();
 }
 
 // =============================================================================

@@ -103,7 +103,8 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     const VehicleConst& vc = VONE ? pk.vc0 : pk.vc[v];
     if (VONE && b == 0) {   // hand vc0 to the finalize (it reads vc[v])
         constexpr int kVCW = (int)(sizeof(VehicleConst) / 4);
-        for (int i = tid; i < kVCW; i += NT) ((int*)pk.vc)[i] = ((const int*)&pk.vc0)[i];
+        for (int i = tid; i < kVCW; i += NT)   // (written through: k_rollout's drain_stores)
+            __hip_atomic_store((int*)pk.vc + i, ((const int*)&pk.vc0)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- phase 1, all waves: u_prev and the (16 x H) noise tile into LDS.  Noise
     //      (standard_normal_noise.py:22-29 / drone_mppi.py:40-44): the 4 normals of (k, t)
@@ -159,7 +160,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     }
     if (tid < H * kQA) u_t[tid] = u_r;
     __syncthreads();
-    if (wid >= NWD) return;
+    if (wid >= NWD) { drain_stores(); return; }
 
     // ---- phase 2, wave 0: the sequential dynamics, lane = (rollout r, axis j).  Lane 3
     //      follows axis 2 bit for bit and lanes past K replicate sample K-1, so every lane
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
         if (lane == 0) { wred[wid][1] = eta; wred[wid][2] = eta2; }
         if (wid > 0 && lane < H) part[wid][lane] = make_float4(n[0], n[1], n[2], n[3]);
         __syncthreads();
-        if (wid != 0) return;
+        if (wid != 0) { drain_stores(); return; }
         eta = 0.0f; eta2 = 0.0f;
 #pragma unroll
         for (int w = 0; w < NWD; ++w) { eta += wred[w][1]; eta2 += wred[w][2]; }
@@ -305,13 +306,14 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
         }
     }
     if (lane == 0)
-        *reinterpret_cast<float4*>(p.hdr + ((size_t)v * p.nb + b) * 4) = make_float4(rho, eta, eta2, nanf);
+        wt_store4(uniform_ptr(p.hdr), ((uint32_t)v * (uint32_t)p.nb + (uint32_t)b) * 16u, make_float4(rho, eta, eta2, nanf));
     if (lane < H) {
-        float* const rdata_v = p.rdata + (size_t)v * kQA * p.nb * H;
+        float* const rdata_v = uniform_ptr(p.rdata + (size_t)v * kQA * p.nb * H);
 #pragma unroll
         for (int a = 0; a < kQA; ++a)
             wt_store(rdata_v, (((uint32_t)a * (uint32_t)p.nb + (uint32_t)b) * (uint32_t)H + (uint32_t)lane) * 4u, n[a]);
     }
+    drain_stores();
 }
 
 extern "C" int mppi_launch_rollout_quad(const DevParams* p, int threads, void* stream) {
