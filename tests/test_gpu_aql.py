@@ -65,6 +65,7 @@ CASES = [
     ("drone", dict(n_samples=4096, n_horizon=32)),
     ("wholebody", dict(n_samples=8192, n_horizon=64)),                 # the C4 shard shape, one group per wave
     ("wholebody", dict(n_samples=32768, n_horizon=64)),                # several groups per wave
+    ("wholebody", dict(n_samples=65536, n_horizon=64)),                # C4 on one GPU: more blocks than fit at once
     ("quadrotor", dict(n_samples=1024, n_horizon=32)),
     ("arm", dict(n_samples=1024, n_horizon=32, cost_terms=("covar", "center", "action"))),   # extended kernel
 ]
