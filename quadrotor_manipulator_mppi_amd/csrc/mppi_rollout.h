@@ -682,10 +682,13 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     const float* usrc = u_prev + (size_t)v * HA;
     float ur[4];
     int jr[2];
+    {   // through a buffer resource over this vehicle's u_prev: 32-bit offsets, and the rows past
+        // H*A read 0 from the range check (no per-load branch, no 64-bit address math)
+        const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(usrc), 0, (MPPI_KO & 128) ? 0 : HA * 4, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = tid + j * nthr;
-        ur[j] = (i < HA && !(MPPI_KO & 128)) ? usrc[i] : 0.0f;
+        for (int j = 0; j < 4; ++j)
+            ur[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(urs, (tid + j * nthr) * 4, 0, 0));
     }
     if (MODEL != MPPI_MODEL_DRONE) {
         const int* js = (const int*)jtab;
@@ -1190,9 +1193,17 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         rws[w] = wsh[w * wstride];
         rho_b = fminf(rho_b, rws[w]);
     }
+    // f_w = exp(-(rho_w - rho_b)/lambda): lane w evaluates wave w's, every lane reads all 8 back
+    // (one transcendental per lane instead of eight)
     float fw[8];
+    {
+        float mine = INFINITY;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) fw[w] = (rws[w] < INFINITY) ? __expf(p.coef * (rws[w] - rho_b)) : 0.0f;
+        for (int w = 0; w < 8; ++w) mine = ((lane & 7) == w) ? rws[w] : mine;
+        const float f = (mine < INFINITY) ? __expf(p.coef * (mine - rho_b)) : 0.0f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) fw[w] = read_lane_f32(f, w);
+    }
     STAMP(12);
     if (tid == 0) {
         float eta = 0.0f, eta2 = 0.0f, nanf = 0.0f;
@@ -1218,9 +1229,9 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         float s = 0.0f;
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
-            float sw = 0.0f;
+            float sw = wsh[w * wstride + 4 + (c * 64 + tl) * NA + a];
 #pragma unroll
-            for (int sg = 0; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
+            for (int sg = 1; sg < R; ++sg) sw += wsh[w * wstride + 4 + (c * 64 + sg * LSEG + tl) * NA + a];
             s += fw[w] * sw;
         }
         wt_store(rdata_v, (rbase + (uint32_t)a * rstride + (uint32_t)t) * 4u, s);
