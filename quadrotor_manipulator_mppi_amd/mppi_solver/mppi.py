@@ -77,6 +77,8 @@ class MPPI:
         self._engine: Optional[Engine] = None
         self._u_prev_host = np.zeros((self.n_horizon, self.n_action), np.float32)
         self.cnt = 0
+        self._row = np.zeros(21, np.float64)   # base xyzquat(7) + q(7) + qdot(7)
+        self._last_target = None               # (engine, pos, quat) last written (_sync_target)
 
     # -------------------------------------------------------------- engine
     def _ensure_engine(self, f64: bool, noise: Optional[str] = None) -> Engine:
@@ -123,15 +125,28 @@ class MPPI:
             return self._q.copy(), self._qdot.copy(), self.base_pose.copy(), self._f64
 
     def _state_row(self, q, qd, base):
-        return np.concatenate([np.asarray(base, np.float64), np.asarray(q, np.float64),
-                               np.asarray(qd, np.float64)])
+        row = self._row   # the engine copies it in mppi_step: one preallocated row
+        row[:7] = base
+        row[7:14] = q
+        row[14:21] = qd
+        return row
+
+    def _sync_target(self, eng: Engine) -> None:
+        """The target into the engine when it changed since the last call (the control call's
+        host time: a target write rebuilds the vehicle constants through one more C call)."""
+        pos = self.target_pose.pose.numpy()
+        quat = self.target_pose.orientation.numpy()
+        last = self._last_target
+        if last is None or last[0] is not eng or not (np.array_equal(last[1], pos) and np.array_equal(last[2], quat)):
+            eng.set_target(pos, quat)
+            self._last_target = (eng, pos.copy(), quat.copy())
 
     def compute_control_input(self, noise: Optional[np.ndarray] = None):
         """mppi.py:122-169.  ``noise`` (K,H,A) switches to injected-noise mode
         (parity with the reference's torch.randn draws)."""
         q, qd, base, f64 = self._snapshot()
         eng = self._ensure_engine(f64, "injected" if noise is not None else None)
-        eng.set_target(self.target_pose.pose.numpy(), self.target_pose.orientation.numpy())
+        self._sync_target(eng)
         out, u0, stats = eng.step(self._state_row(q, qd, base), noise)
         dt = np.float64 if f64 else np.float32
         self.qdes = out[0, :7].astype(dt)
