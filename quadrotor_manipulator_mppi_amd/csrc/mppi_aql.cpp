@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -399,21 +400,23 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 // One kernel-dispatch packet: body first, then header + setup in one release store (the
 // packet processor may read the slot as soon as the header says KERNEL_DISPATCH).
 // Packet fence scopes (0 none, 1 agent, 2 system): rollout acquire, rollout release, finalize
-// acquire, finalize release (a batch's last finalize releases at system scope).  What one
-// kernel of the step reads from the other is written through at device scope and drained
-// before the writing waves end: the rollouts' record bodies, headers and handed-over vehicle
-// constants (mppi_rollout.h drain_stores), the finalize's u_prev.  So neither packet carries
-// a release, whose end-of-kernel L2 writeback cost up to ~0.8 us per C3 step
+// acquire, finalize release.  What one kernel of the step reads from the other is written
+// through at device scope and drained before the writing waves end (the rollouts' record
+// bodies, headers and handed-over vehicle constants, mppi_rollout.h drain_stores; the
+// finalize's u_prev), and read with device-scope loads that bypass the L1 (mppi_device.h
+// ld_dev / kAuxDev).  So no packet of a batch needs a release, whose end-of-kernel L2
+// writeback cost up to ~0.8 us per C3 step, and only a submission's FIRST packet acquires
+// (agent scope: what the host and the HIP stream wrote since the last batch -- argument
+// blocks, state, target), which saves ~0.28 us per C3 step over an acquire on every packet
 // (tools/aql_fence_probe.py).  What stays dirty in the L2s (the costs S, the readback copies
-// of w_eps) is only read after a batch, behind its system-scope release, and every line of it
-// is written by the same block, hence the same XCD, at every step.  Every acquire stays at
-// agent scope (it invalidates the lines an earlier step left in the L2s: the records, u_prev).
-// Diagnostics: MPPI_AQL_FENCES = four digits.
+// of w_eps) is only read after a batch, behind its last finalize's system-scope release, and
+// every line of it is written by the same block, hence the same XCD, at every step.
+// Diagnostics: MPPI_AQL_FENCES = four digits for the packets after the first.
 static int g_fence[4] = {-1, -1, -1, -1};
 static void load_fences() {
     if (g_fence[0] >= 0) return;
     const char* f = getenv("MPPI_AQL_FENCES");
-    const char* def = "1010";
+    const char* def = "0000";
     for (int i = 0; i < 4; ++i) g_fence[i] = (f && strlen(f) == 4 && f[i] >= '0' && f[i] <= '2') ? f[i] - '0' : def[i] - '0';
 }
 static const int kScope[3] = {HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_SYSTEM};
@@ -458,7 +461,7 @@ int step_dispatch(Step* s, int n, std::string* err) {
     load_fences();
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
-        put(s->q, s->kr, s->roll, ra, none, g_fence[0], g_fence[1]);
+        put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
         put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
         // the doorbell takes the index of the last packet written
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
@@ -521,7 +524,7 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     s->call_unread = true;
     const hsa_signal_t none{0};
     load_fences();
-    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, g_fence[0], g_fence[1]);
+    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
     put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
     hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     return 0;

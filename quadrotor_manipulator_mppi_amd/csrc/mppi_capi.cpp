@@ -1471,12 +1471,14 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
 }
 
 // why this engine's mppi_run_steps cannot go native (nullptr: it can)
-static const char* aql_ineligible(const mppi_engine* e) {
+// A batch (mppi_run_steps) may carry the stamps / no-flag diagnostics natively (the timeline
+// build measures the native step that way); a control call waits on the flags, so it may not.
+static const char* aql_ineligible(const mppi_engine* e, bool batch = false) {
     if (e->aql_mode == 0) return "MPPI_DISPATCH=hip";
     if (sharded(e)) return "sharded step (its collective runs on the HIP stream)";
     if (e->timing) return "per-launch timing events (mppi_enable_timing)";
-    if (e->d_stamps) return "stamps diagnostics";
-    if (e->out_dbg || e->no_flag_dbg) return "output diagnostics";
+    if (e->d_stamps && !batch) return "stamps diagnostics";
+    if (e->out_dbg || (e->no_flag_dbg && !batch)) return "output diagnostics";
     return nullptr;
 }
 
@@ -1504,7 +1506,7 @@ static bool aql_ready(mppi_engine* e) {
 
 static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     *used = false;
-    if (const char* why = aql_ineligible(e)) { e->aql_why = why; return MPPI_OK; }
+    if (const char* why = aql_ineligible(e, true)) { e->aql_why = why; return MPPI_OK; }
     if (!aql_ready(e)) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str()) : MPPI_OK;
     HIP_TRY(hipSetDevice(e->cfg.device));
     static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: host phase times

@@ -29,6 +29,27 @@ __device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg
     return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
 }
 
+// Loads of what one kernel of a step hands the next (record bodies and headers, u_prev, the
+// handed-over vehicle constants): device scope (sc1), past this CU's L1.  The producers write
+// these through at device scope and drain their stores (mppi_rollout.h drain_stores), so a
+// native batch's packets after its first need no acquire fence (mppi_aql.cpp): nothing a
+// kernel reads from its predecessor can come from a stale L1 line.
+template <typename T>
+__device__ __forceinline__ T ld_dev(const T* p) {
+    return __hip_atomic_load((const __attribute__((address_space(1))) T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kAuxDev = 16;   // the same for buffer loads (cache-policy operand: sc1)
+
+// A pointer the compiler keeps in SGPRs (its halves read from the first lane): built from
+// kernel arguments through 64-bit VALU math it can land in VGPRs, and a buffer resource over
+// it then becomes a waterfall loop around every load or store.
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic
 // (lgkmcnt) but NOT for its outstanding global stores (vmcnt), which
 // __syncthreads() would drain -- nothing in these kernels reads its own

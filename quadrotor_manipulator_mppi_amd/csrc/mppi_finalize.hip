@@ -27,7 +27,7 @@ constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 wa
 constexpr int kMaxRec = 4096;
 // timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
 // outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor), 32 skips
-// the u_prev update, 64 skips the tail parameters' kernel-argument loads
+// the u_prev update, 64 skips the tail parameters' kernel-argument loads, 128 the final drain
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
@@ -114,8 +114,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(0);
     const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
     const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
-    const float* hdr = hdr_base + (size_t)v * (uint32_t)hdr_vs;
-    const float* col = dat_base + (size_t)v * (uint32_t)d_vs + (size_t)a * d_as + w0;
+    // (both bases and the header range kept in SGPRs: in a build where the compiler put one
+    // in VGPRs, every record load became a waterfall loop over a "divergent" resource)
+    const float* hdr = uniform_ptr(hdr_base + (size_t)v * (uint32_t)hdr_vs);
+    const float* col = uniform_ptr(dat_base + (size_t)v * (uint32_t)d_vs + (size_t)a * d_as + w0);
     const FinTail& T = *tail;
     const int g = lane / CW, q = lane - g * CW, gr = wv * ROWS + g;
     const bool qv = q < W;
@@ -167,14 +169,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // then the loads that need those pointers (global address space: a flat load also
         // counts in lgkmcnt, so every later scalar wait would wait for it too)
         up += (size_t)v * H * A;
-        using gfloat = const __attribute__((address_space(1))) float;
-        using gdouble = const __attribute__((address_space(1))) double;
-        if (wv == 0 && q < W && g == 0) u_old = *(gfloat*)(up + (w0 + q) * A + a);
+        // (device-scope loads: the previous finalize's u_prev, the rollout's handed-over vc)
+        if (wv == 0 && q < W && g == 0) u_old = ld_dev(up + (w0 + q) * A + a);
         if (tid == 0 && sl == 0) {
             const VehicleConst* vcp = vcb + v;
-            x0f = *(gfloat*)(vcp->pos0f + a); v0f = *(gfloat*)(vcp->vel0f + a);
-            x0d = *(gdouble*)(vcp->pos0 + a); v0d = *(gdouble*)(vcp->vel0 + a);
-            if (seq == kSeqFromVc) seqv = *(const __attribute__((address_space(1))) uint32_t*)(vcp->_pad);
+            x0f = ld_dev(vcp->pos0f + a); v0f = ld_dev(vcp->vel0f + a);
+            x0d = ld_dev(vcp->pos0 + a); v0d = ld_dev(vcp->vel0 + a);
+            if (seq == kSeqFromVc) seqv = ld_dev((const uint32_t*)vcp->_pad);   // (its bits)
         }
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
@@ -189,7 +190,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // their offsets run past the resources' ranges, which read 0 instead of faulting.
     const uint32_t hrs_b = (uint32_t)hdr_rs * 4u, drs_b = (uint32_t)d_rs * 4u;
     const __amdgpu_buffer_rsrc_t hrsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hdr), 0, (int)((uint32_t)n * hrs_b), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hdr), 0, __builtin_amdgcn_readfirstlane((int)((uint32_t)n * hrs_b)),
+                                          0x00020000);
     // (the range is block-uniform, but its W reaches the compiler through VGPR math: without
     // readfirstlane every body load became a waterfall loop over a "divergent" resource)
     const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -206,9 +208,9 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
 #pragma unroll
         for (int i = 0; i < kNPT; ++i) {
             okm |= (uint32_t)(r0 + (uint32_t)(i * TR) < (uint32_t)n) << i;
-            const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(hrsrc, (int)(hoff + (uint32_t)(i * TR) * hrs_b), 0, 0);
+            const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(hrsrc, (int)(hoff + (uint32_t)(i * TR) * hrs_b), 0, kAuxDev);
             hd[i] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
-            xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crsrc, (int)(coff + (uint32_t)(i * TR) * drs_b), 0, 0));
+            xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crsrc, (int)(coff + (uint32_t)(i * TR) * drs_b), 0, kAuxDev));
         }
         if (base == 0 && !(MPPI_FIN_KO & 64)) {   // (64: timing knockout, tail parameters not loaded)
             __builtin_amdgcn_sched_barrier(0);   // the first chunk's record loads issue first
@@ -392,7 +394,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     }
     FSTAMP(6);
     FSTAMPRT(14);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!(MPPI_FIN_KO & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only

@@ -24,7 +24,7 @@
 // wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain,
 // 8 the pose cost, 16 the trajectory stores, 32 Box-Muller, 64 the block record body,
 // 128 the u_prev loads (H*A <= 4 * block threads), 256 the prologue's block barrier (LDS
-// staging read unsynchronised).
+// staging read unsynchronised), 512 the end-of-wave store drain (the hand-off unordered).
 #ifndef MPPI_KO
 #define MPPI_KO 0
 #endif
@@ -394,7 +394,7 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
     do {                                                                                              \
         __builtin_amdgcn_sched_barrier(0);                                                            \
         if (pk.stamps && lane == 0) {                                                                 \
-            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            const size_t w_ = ((size_t)blockIdx.y * p.nb + blockIdx.x) * nw + wid;        \
             pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memtime();                             \
         }                                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                            \
@@ -412,7 +412,7 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
     do {                                                                                              \
         __builtin_amdgcn_sched_barrier(0);                                                            \
         if (pk.stamps && lane == 0) {                                                                 \
-            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            const size_t w_ = ((size_t)blockIdx.y * p.nb + blockIdx.x) * nw + wid;        \
             pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
             if ((i) == 13) /* where the wave ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4) */        \
                 pk.stamps[w_ * kStamps + 15] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
@@ -427,7 +427,7 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 #define STAMP(i)                                                                                      \
     do {                                                                                              \
         if (((i) == 1 || (i) == 5 || (i) == 10) && pk.stamps && lane == 0) {                          \
-            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            const size_t w_ = ((size_t)blockIdx.y * p.nb + blockIdx.x) * nw + wid;        \
             pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
         }                                                                                             \
     } while (0)
@@ -435,7 +435,7 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 #define STAMPRT(i)                                                                                    \
     do {                                                                                              \
         if (pk.stamps && lane == 0) {                                                                 \
-            const size_t w_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wid; \
+            const size_t w_ = ((size_t)blockIdx.y * p.nb + blockIdx.x) * nw + wid;        \
             pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
             if ((i) == 13)                                                                            \
                 pk.stamps[w_ * kStamps + 15] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
@@ -502,21 +502,14 @@ __device__ __forceinline__ void wt_store4(float* base_uniform, uint32_t byte_off
     const u32x4 v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)byte_off, 0, MPPI_REC_AUX);
 }
-// A pointer the compiler keeps in SGPRs (its halves read from the first lane): built from
-// kernel arguments through 64-bit VALU math it lands in VGPRs, and a buffer resource over it
-// became a waterfall loop around every store.
-template <typename T>
-__device__ __forceinline__ T* uniform_ptr(T* p) {
-    const uint64_t a = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return (T*)(((uint64_t)hi << 32) | lo);
-}
 // The rollout's outputs the finalize reads (record bodies and headers, and the vehicle
 // constants block 0 hands over) are written through at device scope; every wave waits for its
 // stores before it ends.  So they are visible device-wide when the kernel completes, and the
 // native dispatch's rollout packet needs no release fence (the end-of-kernel L2 writeback,
 // ~0.8 us per step at C3; mppi_aql.cpp).
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void drain_stores() {
+    if (!(MPPI_KO & 512)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // fp32 inclusive scans of NA independent dims inside L-lane segments, step-major
 // (the DPP wait states of one dim are filled by the others).  Each step is one
@@ -688,7 +681,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             const_cast<float*>(usrc), 0, (MPPI_KO & 128) ? 0 : HA * 4, 0x00020000);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            ur[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(urs, (tid + j * nthr) * 4, 0, 0));
+            ur[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(urs, (tid + j * nthr) * 4, 0, kAuxDev));
     }
     if (MODEL != MPPI_MODEL_DRONE) {
         const int* js = (const int*)jtab;

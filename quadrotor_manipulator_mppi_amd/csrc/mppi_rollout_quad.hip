@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     // u_prev (H*4 <= 256 floats, one per thread) stays in flight across the draws, and the
     // dynamics phase's scalars are read here, so their loads share the noise phase's wait
     const float* up = u_prev + (size_t)v * H * kQA;
-    const float u_r = (tid < H * kQA) ? up[tid] : 0.0f;
+    const float u_r = (tid < H * kQA) ? ld_dev(up + tid) : 0.0f;   // (the previous finalize's; device scope)
     float x6[6], v6[6], tg3[3], ii3[3];
 #pragma unroll
     for (int d = 0; d < 6; ++d) { x6[d] = uniform_f32(vc.pos0f[d]); v6[d] = uniform_f32(vc.vel0f[d]); }

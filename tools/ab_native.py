@@ -4,7 +4,7 @@
 
 Each build is loaded into the one process (RTLD_LOCAL; its code objects next to it), one engine
 per (build, workload); per rep and build: a 50-step priming batch, then the wall time of a
-`steps` batch (default 500, MPPI_AB_STEPS) and of 20 control calls.  Prints the median us per
+`steps` batch (default 500, MPPI_AB_STEPS) and of 20 control calls (MPPI_AB_CALLS).  Prints the median us per
 step and per call and their inter-quartile ranges."""
 import ctypes as C
 import os
@@ -36,6 +36,7 @@ def main():
     runs = [r.split() for r in sys.argv[2].split(";") if r.strip()]
     libs = sys.argv[3:]
     steps = int(os.environ.get("MPPI_AB_STEPS", "500"))
+    ncalls = int(os.environ.get("MPPI_AB_CALLS", "20"))   # 0 for builds without completion flags (knockouts)
     eng = {}
     for li, p in enumerate(libs):
         capi._lib = load(p)
@@ -64,8 +65,8 @@ def main():
                 e.run_steps(steps)
                 e.synchronize()
                 t1 = time.perf_counter()
-                calls = []
-                for _ in range(20):
+                calls = [0.0]
+                for _ in range(ncalls):
                     c0 = time.perf_counter()
                     e.step(st)
                     calls.append(time.perf_counter() - c0)

@@ -34,5 +34,5 @@ for _ in range(5):
     a.run_steps(1000)
     a.synchronize()
     rates.append((time.perf_counter() - t0) / 1000 * 1e6)
-print(f"fences={os.environ.get('MPPI_AQL_FENCES', 'default 1010')} bit-exact vs HIP after 300 steps: {ok}  "
+print(f"fences={os.environ.get('MPPI_AQL_FENCES', 'default 0000')} bit-exact vs HIP after 300 steps: {ok}  "
       f"us/step (1000-step batches): median {np.median(rates):.2f}  all {[round(x, 2) for x in rates]}")

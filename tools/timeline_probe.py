@@ -44,6 +44,13 @@ def main():
     fb = np.zeros((4096, 16), np.uint64)
     se.run_steps(50)
     eng.synchronize()
+    import time
+    periods = []   # the step period of this build (the stamps' own cost included)
+    for _ in range(5):
+        t0 = time.perf_counter()
+        se.run_steps(500)
+        eng.synchronize()
+        periods.append((time.perf_counter() - t0) / 500 * 1e9)
     rows = []
     for _ in range(trials):
         se.run_steps(10)
@@ -87,7 +94,8 @@ def main():
         rows.append(row)
     keys = rows[0].keys()
     med = {k: float(np.median([r[k] for r in rows if k in r])) for k in keys}
-    out = {"workload": name, "trials": trials, "ns_median": {k: round(v) for k, v in med.items()}}
+    out = {"workload": name, "trials": trials, "dispatch": eng.dispatch_info(),
+           "ns_median": {k: round(v) for k, v in med.items()}}
     if "final_start" in med:
         gaps = {"rollout_span": med["roll_end"]}
         prev = med["roll_end"]
@@ -98,6 +106,8 @@ def main():
         gaps["gap_to_final"] = med["final_start"] - prev
         gaps["final_span"] = med["final_end"] - med["final_start"]
         gaps["step_to_final_end"] = med["final_end"]
+        gaps["step_period"] = float(np.median(periods))
+        gaps["gap_final_to_next_rollout"] = gaps["step_period"] - med["final_end"]
         out["us"] = {k: round(v / 1e3, 3) for k, v in gaps.items()}
     print(json.dumps(out), flush=True)
     eng.close()
