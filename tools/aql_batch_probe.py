@@ -40,12 +40,22 @@ for rep in range(15):
             e.run_steps(n)
             t1 = time.perf_counter()
             e.synchronize()
+            ts = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            res[m].setdefault(n, []).append(((t2 - t0) * 1e6, (t1 - t0) * 1e6))
+            e.synchronize()          # both again, idle: the bracket's own host cost
+            ti = time.perf_counter()
+            torch.cuda.synchronize()
+            tj = time.perf_counter()
+            res[m].setdefault(n, []).append(((t2 - t0) * 1e6, (t1 - t0) * 1e6, (ts - t1) * 1e6, (t2 - ts) * 1e6,
+                                             (ti - t2) * 1e6, (tj - ti) * 1e6))
 for m in engines:
     tot = [np.median([x[0] for x in res[m][n]]) for n in ns]
     enq = [np.median([x[1] for x in res[m][n]]) for n in ns]
     slope, icpt = np.polyfit(ns, tot, 1)
     print(f"{m}: " + "  ".join(f"n={n}: {t:.1f} us (enq {q:.1f})" for n, t, q in zip(ns, tot, enq)) +
           f"  | fit: {slope:.2f} us/step + {icpt:.1f} us per batch; n=20 -> {tot[ns.index(20)] / 20:.2f} us/step")
+    for n in (1, 20):
+        med = np.median(np.array(res[m][n]), axis=0)
+        print(f"  {m} n={n}: run_steps call {med[1]:.1f}, engine sync {med[2]:.1f}, torch sync {med[3]:.1f} us; "
+              f"idle: engine sync {med[4]:.1f}, torch sync {med[5]:.1f} us")
