@@ -132,6 +132,41 @@ def test_native_is_the_default(monkeypatch):
     e.close()
 
 
+def test_native_sees_host_writes_between_batches(monkeypatch):
+    """Only a native submission's first packet acquires (mppi_aql.cpp); everything the host
+    or the HIP stream writes between batches -- target, u_prev, state, the step counter, a
+    HIP-path step in timing mode -- must be seen by the next batch's kernels.  Each change is
+    made on both engines and the batches stay bit-identical with HIP."""
+    h, a = _pair(monkeypatch, "arm", n_samples=2048, n_horizon=32)
+    rng = np.random.default_rng(7)
+    for i in range(4):
+        for e in (h, a):
+            e.run_steps(3)
+        _same(h, a, f"round {i}: batch")
+        tgt = [0.1 + 0.02 * i, 0.4 - 0.01 * i, 1.6]
+        u = rng.normal(0.0, 0.2, (1, h.H, h.A)).astype(np.float32)
+        st = _state("arm", 1, shift=0.01 * (i + 1))
+        for e in (h, a):
+            e.set_target(tgt, [-0.5, -0.5, 0.5, -0.5])
+            e.run_steps(2)
+            e.set_u_prev(u)
+            e.run_steps(2)
+            e.set_state(st)
+            e.run_steps(1)
+            e.set_step_counter(100 + 7 * i)
+            e.run_steps(2)
+        _same(h, a, f"round {i}: after host writes")
+    for e in (h, a):   # a HIP-path batch in between (timing mode), then native again
+        e.enable_timing(True)
+        e.run_steps(2)
+        e.synchronize()
+        e.enable_timing(False)
+        e.run_steps(3)
+    _same(h, a, "after a HIP-path batch")
+    h.close()
+    a.close()
+
+
 CALL_CASES = [("arm", dict(n_samples=4096, n_horizon=32)), ("arm", dict(n_samples=1024, n_horizon=32, state_f64=False)),
               ("drone", dict(n_samples=4096, n_horizon=32)), ("wholebody", dict(n_samples=8192, n_horizon=64)),
               ("quadrotor", dict(n_samples=1024, n_horizon=32))]
