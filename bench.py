@@ -472,6 +472,31 @@ def secondary_entry(s, ns):
     return e
 
 
+def dropin_latency(n_calls):
+    """The reference's own control call through the drop-in class (mppi_solver/mppi.py MPPI,
+    the kinova node's tick: update_joint from the joint-state callback, then
+    compute_control_input -> (qdes, vdes) numpy), arm C3 shape with an fp64 state, device
+    noise: host-inclusive wall time per call, p50/p99 over n_calls after 20 untimed."""
+    import torch
+    from quadrotor_manipulator_mppi_amd.mppi_solver.mppi import MPPI
+    m = MPPI(n_samples=4096, n_horizon=32, verbose=False)
+    q = torch.tensor([0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0], dtype=torch.float64)
+    v = torch.zeros(13, dtype=torch.float64)
+    lat = []
+    for i in range(n_calls + 20):
+        t0 = time.perf_counter()
+        m.update_joint(q, v)
+        qdes, vdes = m.compute_control_input()
+        if i >= 20:
+            lat.append(time.perf_counter() - t0)
+    assert np.isfinite(qdes).all() and np.isfinite(vdes).all()
+    m._engine.close()
+    lat = np.array(lat) * 1e3
+    return {"p50_ms": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)), "calls": int(lat.size),
+            "what": "drop-in MPPI.update_joint + compute_control_input (mppi.py:196-200, :122-169), K=4096 H=32, "
+                    "fp64 state, device noise, host-inclusive"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -542,6 +567,10 @@ def main():
             s = run_workload(wname, ns, 20, 1, None, 50, batches=3)
             secondary[wname] = secondary_entry(s, ns)
             log(f"secondary {wname}: {secondary[wname]}")
+    dropin = None
+    if world == 1 and workload == "arm_c3" and args.latency_steps:
+        dropin = dropin_latency(args.latency_steps)
+        log(f"drop-in latency: {dropin}")
     cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, cpu_all = cpu_baseline(workload, args.cpu_budget)
@@ -553,6 +582,8 @@ def main():
             log(f"measured HBM: {measured}")
         line = make_line(workload, r, args, secondary, cpu, cpu_all, measured)
         line["host_binding"] = binding
+        if dropin is not None:
+            line["dropin_latency"] = dropin
         print(json.dumps(line), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()

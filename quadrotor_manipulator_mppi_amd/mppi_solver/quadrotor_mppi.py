@@ -40,6 +40,8 @@ class MPPI:
         self.sigma = torch.diag(torch.tensor([30.0, 1.0, 1.0, 1.0]))
         self.param_lambda = 0.1
         self.target = [1.0, 2.0, 3.4]          # drone_mppi.py:141
+        self._row = np.zeros(12, np.float64)   # x(6) + v(6) of the control call
+        self._last_target = None               # (engine, target bytes) last written
         self.params = dict(quad_mass=mass, quad_inertia=tuple(inertia), quad_kd=kd, quad_gravity=gravity)
         self.verbose = verbose
         self._noise, self._seed = noise, seed
@@ -83,11 +85,20 @@ class MPPI:
             self.v_prev = torch.tensor(np.asarray(v, np.float64).reshape(6), dtype=torch.float32)
 
     def compute_control_input(self, noise: Optional[np.ndarray] = None):
+        row = self._row   # x, v into one preallocated fp64 row (the engine copies it)
         with self._lock:
-            x, v = self.x_prev.numpy().copy(), self.v_prev.numpy().copy()
+            row[:6] = self.x_prev.numpy()
+            row[6:] = self.v_prev.numpy()
         eng = self._ensure_engine("injected" if noise is not None else self._noise)
-        eng.set_target(np.asarray(self.target, np.float32))
-        out, u0, stats = eng.step(np.concatenate([x, v]).astype(np.float64), noise)
+        # the target into the engine only when it changed (a target write rebuilds the
+        # vehicle constants through one more C call)
+        tgt = np.asarray(self.target, np.float32)
+        key = tgt.tobytes()
+        last = self._last_target
+        if last is None or last[0] is not eng or last[1] != key:
+            eng.set_target(tgt)
+            self._last_target = (eng, key)
+        out, u0, stats = eng.step(row, noise)
         self.u = torch.from_numpy(u0[0].copy())
         self.last_stats = stats[0]
         if self.verbose:

@@ -410,6 +410,42 @@ def test_dropin_arm_class_reference_call_pattern():
         assert np.isfinite(q).all() and np.isfinite(v).all()
 
 
+def test_dropin_target_changes_reach_the_engine():
+    """The drop-ins write the target into the engine only when it changed (mppi.py
+    _sync_target, drone_mppi.py): a tensor modified in place, a tensor or Pose field
+    reassigned, and a drone target list edited in place must each reach the next call."""
+    from quadrotor_manipulator_mppi_amd.mppi_solver.mppi import MPPI
+    from quadrotor_manipulator_mppi_amd.mppi_solver.drone_mppi import MPPI as DroneMPPI
+    g = load_golden("arm_k100_h32_f64.npz")
+    n = g["s0_noise"]
+    a, b, c = MPPI(verbose=False), MPPI(verbose=False), MPPI(verbose=False)
+    for m in (a, b, c):
+        m.update_joint(g["q_full"], g["v_full"])
+        m.compute_control_input(noise=n)
+    a.target_pose.pose[0] += 0.05                                   # in place
+    b.target_pose.pose = b.target_pose.pose + torch.tensor([0.05, 0.0, 0.0])   # reassigned
+    qa, _ = a.compute_control_input(noise=n)
+    qb, _ = b.compute_control_input(noise=n)
+    qc, _ = c.compute_control_input(noise=n)                        # target unchanged
+    np.testing.assert_array_equal(qa, qb)
+    assert not np.array_equal(qa, qc)
+    a.target_pose.orientation = torch.tensor([0.0, 0.0, 0.0, 1.0])  # reassigned
+    b.target_pose.orientation[:] = torch.tensor([0.0, 0.0, 0.0, 1.0])   # in place
+    np.testing.assert_array_equal(a.compute_control_input(noise=n)[0], b.compute_control_input(noise=n)[0])
+
+    gd = load_golden("drone_k128_h20.npz")
+    d1, d2 = DroneMPPI(n_samples=128, n_timestep=20), DroneMPPI(n_samples=128, n_timestep=20)
+    for m in (d1, d2):
+        m.verbose = False
+        m.set_state(gd["s0_x_in"].tolist(), gd["s0_v_in"].tolist())
+        m.compute_control_input(noise=gd["s0_noise"])
+    d1.target[0] = 1.5                                              # list edited in place
+    d2.target = [1.5, 2.0, 3.4]                                     # reassigned
+    x1, _ = d1.compute_control_input(noise=gd["s1_noise"])
+    x2, _ = d2.compute_control_input(noise=gd["s1_noise"])
+    np.testing.assert_array_equal(x1.cpu().numpy(), x2.cpu().numpy())
+
+
 def test_dropin_drone_class_reference_call_pattern():
     from quadrotor_manipulator_mppi_amd.mppi_solver.drone_mppi import MPPI
     g = load_golden("drone_k128_h20.npz")
