@@ -472,6 +472,11 @@ int step_dispatch(Step* s, int n, std::string* err) {
 int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
               uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err) {
     if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
+    static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: phases of a call
+    static double pacc[4] = {0, 0, 0, 0};
+    static long pcn = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto p0 = now();
     Kern kr, kf;
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -508,7 +513,9 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     memcpy(tmp + seq_off, seq, 4);
     const uint32_t nb = (roll.arg_bytes + 63) & ~63u;   // whole 64 B lines
     memset(tmp + roll.arg_bytes, 0, nb - roll.arg_bytes);
+    const auto p1 = now();
     memcpy(blk, tmp, nb);
+    const auto p2 = now();
     if (s->call_vis) {
         // device memory written through the BAR: drain the write-combining buffers, flush the
         // host data path and read the flush register back (the writes have landed) before the
@@ -519,6 +526,7 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
         (void)*f;
     }
     std::atomic_thread_fence(std::memory_order_release);
+    const auto p3 = now();
     hsa_signal_add_relaxed(s->done, 1);
     ++s->outstanding;
     s->call_unread = true;
@@ -527,6 +535,16 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
     put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
     hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
+    if (prof) {
+        const auto p4 = now();
+        pacc[0] += std::chrono::duration<double, std::micro>(p1 - p0).count();
+        pacc[1] += std::chrono::duration<double, std::micro>(p2 - p1).count();
+        pacc[2] += std::chrono::duration<double, std::micro>(p3 - p2).count();
+        pacc[3] += std::chrono::duration<double, std::micro>(p4 - p3).count();
+        if (++pcn % 1000 == 0)
+            fprintf(stderr, "[mppi aql] step_call (us): lookups+checks %.2f  block write %.2f  flush+readback %.2f  packets %.2f\n",
+                    pacc[0] / pcn, pacc[1] / pcn, pacc[2] / pcn, pacc[3] / pcn);
+    }
     return 0;
 }
 

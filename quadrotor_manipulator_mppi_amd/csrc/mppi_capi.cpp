@@ -375,6 +375,7 @@ struct mppi_engine {
     bool aql_out = false;               // the pending outputs come from a native batch
     bool aql_call = false;              // ... from a native control call (flags carry bit 31)
     bool calls_native = false;          // the last mppi_step went out as native packets
+    double call_wait_us = 0.0;          // diagnostics (MPPI_AQL_PROFILE): the last call's flag wait
 };
 
 namespace {
@@ -1352,6 +1353,7 @@ static mppi_status wait_outputs(mppi_engine* e) {
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         mppi_aql::step_call_read(e->aql);
+        e->call_wait_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         return MPPI_OK;
     }
     if (!e->event_wait) {
@@ -1449,9 +1451,25 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
     mppi_status st;
     if (e->cfg.noise_mode == MPPI_NOISE_PHILOX && e->V == 1 && !sharded(e)) {   // one vehicle: native packets
         bool used = false;
+        static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: host phases of a call
+        const auto c0 = std::chrono::steady_clock::now();
         if ((st = control_call_aql(e, state, &used)) != MPPI_OK) return st;
         e->calls_native = used;
-        if (used) return mppi_read_outputs(e, out, u0, stats);
+        if (used) {
+            if (!prof) return mppi_read_outputs(e, out, u0, stats);
+            const auto c1 = std::chrono::steady_clock::now();
+            st = mppi_read_outputs(e, out, u0, stats);
+            const auto c2 = std::chrono::steady_clock::now();
+            static double acc[3] = {0, 0, 0};
+            static long cn = 0;
+            const double pre = std::chrono::duration<double, std::micro>(c1 - c0).count();
+            const double rd = std::chrono::duration<double, std::micro>(c2 - c1).count();
+            acc[0] += pre; acc[1] += e->call_wait_us; acc[2] += rd - e->call_wait_us;
+            if (++cn % 1000 == 0)
+                fprintf(stderr, "[mppi aql] per call (us): before the doorbell %.2f  flag wait %.2f  outputs + check_reach %.2f\n",
+                        acc[0] / cn, acc[1] / cn, acc[2] / cn);
+            return st;
+        }
     }
     e->calls_native = false;
     if (state && (st = mppi_set_state(e, state)) != MPPI_OK) return st;
