@@ -42,3 +42,30 @@ class OutputRing:
         self._events[i].record()
         self._used[i] = True
         return t
+
+
+class LazyU:
+    """The reference's ``u`` attribute (``self.u = u[0].clone()``, mppi.py:155 /
+    drone_mppi.py:163): a torch tensor, built on its first read after each call from the
+    call's own u0 row (``_set_u0``), so a controller that never reads it does not pay a
+    ``torch.from_numpy`` (~1 us) per control call.  Assigning ``u`` stores the tensor."""
+
+    _u_t = None
+    _u_np = None
+
+    @property
+    def u(self):
+        t = self._u_t
+        if t is None:
+            t = self._u_t = torch.from_numpy(self._u_np)
+        return t
+
+    @u.setter
+    def u(self, value):
+        self._u_t = value
+        self._u_np = None
+
+    def _set_u0(self, row: np.ndarray) -> None:
+        """row: this call's u0 (a fresh array the engine returned, owned from here on)."""
+        self._u_np = row
+        self._u_t = None

@@ -20,10 +20,10 @@ import numpy as np
 import torch
 
 from ..engine import Engine, make_config
-from ._outputs import OutputRing
+from ._outputs import LazyU, OutputRing
 
 
-class MPPI:
+class MPPI(LazyU):
     def __init__(self, n_samples: int = 1000, n_timestep: int = 32, device: Optional[int] = None,
                  noise: str = "philox", seed: int = 0x5EED, verbose: bool = False):
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
@@ -97,7 +97,7 @@ class MPPI:
             eng.set_target(tgt)
             self._last_target = (eng, key)
         out, u0, stats = eng.step(row, noise)
-        self.u = torch.from_numpy(u0[0].copy())
+        self._set_u0(u0[0])   # the tensor is made on first read (LazyU)
         self.last_stats = stats[0]
         if self.verbose:
             print("Rho :", torch.tensor(stats[0].rho))

@@ -27,6 +27,7 @@ import torch
 from ..engine import Engine, host_fk, make_config
 from ..robot.urdf_chain import load_chain, parse_urdf_chain
 from ..utils.pose import Pose
+from ._outputs import LazyU
 
 
 def _is_f64(x) -> bool:
@@ -51,7 +52,7 @@ def _host_view(x, dtype) -> np.ndarray:
     return np.asarray(x, dtype=dtype)
 
 
-class MPPI:
+class MPPI(LazyU):
     def __init__(self, n_samples: int = 100, n_horizon: int = 32, device: Optional[int] = None,
                  noise: str = "philox", seed: int = 0x5EED, urdf_path: Optional[str] = None,
                  root_link: str = "base", end_link: str = "j2s7s300_link_7", verbose: bool = True,
@@ -174,7 +175,7 @@ class MPPI:
         dt = np.float64 if f64 else np.float32
         self.qdes = out[0, :7].astype(dt)
         self.vdes = out[0, 7:14].astype(dt)
-        self.u = torch.from_numpy(u0[0].copy())
+        self._set_u0(u0[0])   # the tensor is made on first read (LazyU)
         self.last_stats = stats[0]
         self.cnt += 1
         if stats[0].reach and self.verbose:   # mppi.py:165-167
