@@ -1,7 +1,8 @@
-"""Interleaved same-process A/B of rollout block sizes on the native path (tools/, not shipped):
-    python tools/ab_geometry.py <reps> "<model K H>;..." <threads> <threads> ...
-One engine per (workload, block size); per rep, in both orders: a 50-step priming batch,
-then the wall time of a 500-step batch.  Prints the median us per step and its IQR."""
+"""Interleaved same-process A/B of rollout launch geometries on the native path (tools/, not shipped):
+    python tools/ab_geometry.py <reps> "<model K H>;..." <threads[:blocks]> <threads[:blocks]> ...
+(blocks = blocks per vehicle, 0 = the engine's automatic choice).  One engine per (workload,
+geometry); per rep, in alternating order: a 50-step priming batch, then the wall time of a
+500-step batch.  Prints the median us per step and its IQR."""
 import os
 import sys
 import time
@@ -19,12 +20,13 @@ STATE = {"arm": [0, 0, 1, 0, 0, 0, 1] + [1.57, 1.7, 0, 4.4, 0, 4.71, 0.0] + [0.0
 def main():
     reps = int(sys.argv[1])
     runs = [r.split() for r in sys.argv[2].split(";") if r.strip()]
-    sizes = [int(x) for x in sys.argv[3:]]
+    sizes = [tuple(int(y) for y in (x.split(":") + ["0"])[:2]) for x in sys.argv[3:]]
     eng = {}
     for r in runs:
         model, K, H = r[0], int(r[1]), int(r[2])
         for t in sizes:
-            e = Engine(make_config(model, n_samples=K, n_horizon=H, state_f64=(model == "arm"), block_threads=t))
+            e = Engine(make_config(model, n_samples=K, n_horizon=H, state_f64=(model == "arm"), block_threads=t[0],
+                                   blocks_per_vehicle=t[1]))
             if model == "drone":
                 e.set_target([1.0, 2.0, 3.4])
             else:
@@ -49,7 +51,8 @@ def main():
         print(" ".join(r))
         for t in sizes:
             q = np.percentile(res[r[0], t], [25, 50, 75])
-            print(f"  block {t:4d}  step {q[1]:7.2f} [{q[0]:6.2f},{q[2]:6.2f}] us  ({eng[r[0], t].dispatch_info()})")
+            print(f"  threads {t[0]:4d} blocks {t[1] or 'auto':>4}  step {q[1]:7.2f} [{q[0]:6.2f},{q[2]:6.2f}] us  "
+                  f"({eng[r[0], t].dispatch_info()})")
     for e in eng.values():
         e.close()
 
