@@ -1593,7 +1593,12 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
     if (aql_ineligible(e) || e->event_wait) return MPPI_OK;
     if (!aql_ready(e)) return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", e->aql_why.c_str())
                                                : MPPI_OK;
+    static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: host phases
+    static double pacc[4] = {0, 0, 0, 0};
+    static long pcn = 0;
+    const auto q0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(e->cfg.device));
+    const auto q1 = std::chrono::steady_clock::now();
     if (state) {   // mppi_set_state's work for one vehicle: host-side constants only
         std::memcpy(e->state.data(), state, sizeof(double) * e->state.size());
         e->state_set = true;
@@ -1601,11 +1606,13 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
         if (st != MPPI_OK) return st;
     }
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_step before mppi_set_state");
+    const auto q2 = std::chrono::steady_clock::now();
     {   // HIP work queued on the engine's stream first (0.1 us when there is none)
         const hipError_t q = hipStreamQuery(e->stream);
         if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(e->stream));
         else if (q != hipSuccess) return fail(MPPI_ERR_HIP, "engine stream: %s", hipGetErrorString(q));
     }
+    const auto q3 = std::chrono::steady_clock::now();
     static thread_local LaunchDesc roll, fin;
     DevParams p = e->dp;
     p.noise_in = nullptr;
@@ -1624,6 +1631,14 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
     }
     mppi_aql::set_capture(nullptr);
     if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
+    if (prof) {
+        const auto q4 = std::chrono::steady_clock::now();
+        const std::chrono::steady_clock::time_point qs[5] = {q0, q1, q2, q3, q4};
+        for (int i = 0; i < 4; ++i) pacc[i] += std::chrono::duration<double, std::micro>(qs[i + 1] - qs[i]).count();
+        if (++pcn % 1000 == 0)
+            fprintf(stderr, "[mppi aql] call setup (us): hipSetDevice %.2f  vehicle constants %.2f  stream query %.2f  "
+                            "capture %.2f\n", pacc[0] / pcn, pacc[1] / pcn, pacc[2] / pcn, pacc[3] / pcn);
+    }
     // the vehicle constants' spare word inside the rollout's last argument (DevParams by value)
     const uint32_t seq_off = roll.arg_bytes - (uint32_t)sizeof(DevParams) + (uint32_t)offsetof(DevParams, vc0) +
                              (uint32_t)offsetof(VehicleConst, _pad);
