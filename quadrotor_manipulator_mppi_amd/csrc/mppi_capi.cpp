@@ -5,6 +5,7 @@
 // the reference builds its tensors, and sequences the two kernels of a step on
 // one HIP stream.  See DESIGN.md for the data layout and the kernel roofline.
 #include <dlfcn.h>
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -322,6 +323,8 @@ struct mppi_engine {
     float* d_noise_in = nullptr;
     uint32_t step_ctr = 0;              // Philox counter word; +1 per finalized step
     uint32_t out_seq = 0;               // completion-flag value of the step read_outputs waits for
+    std::vector<double> rec_out;        // a read step's outputs assembled from its tagged records
+    std::vector<float> rec_u0, rec_stats;
     uint32_t seq_ctr = 0;               // last completion-flag value handed out: monotonic and
                                         // independent of step_ctr (mppi_set_step_counter rewinds that)
     bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
@@ -448,9 +451,11 @@ mppi_status use_device(mppi_engine* e) {
 
 size_t off_u0(const mppi_engine* e) { return ((size_t)e->V * e->out_dim * sizeof(double) + 15) & ~size_t(15); }
 size_t off_stats(const mppi_engine* e) { return (off_u0(e) + (size_t)e->V * e->A * sizeof(float) + 15) & ~size_t(15); }
-// completion flags (V, A) uint32: block (a, slice 0) of vehicle v stores the step's
-// sequence number after its outputs (system-scope release); the host polls them
+// tagged output records of a read step (k_finalize): per vehicle, 2 per dim -- (o1, u0, seq),
+// (o2, nan flag, seq) -- and one (rho, eta, ess, seq), 16 B each, each written by ONE store;
+// the host polls their tags and takes the values from the records themselves
 size_t off_flags(const mppi_engine* e) { return off_stats(e) + (size_t)e->V * 16; }
+size_t rec_count(const mppi_engine* e) { return (size_t)e->V * (2 * e->A + 1); }
 
 mppi_status build_vehicle_consts(mppi_engine* e) {
     const mppi_config& c = e->cfg;
@@ -849,7 +854,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
     if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * traj_floats(e)));
     if (c.store_noise) CREATE_TRY(hipMalloc(&e->d_noise_out, sizeof(float) * KH * e->A));
-    e->out_bytes = (int64_t)(off_flags(e) + (size_t)e->V * e->A * sizeof(uint32_t));
+    e->out_bytes = (int64_t)(off_flags(e) + rec_count(e) * 16);
     CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
     CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocMapped | hipHostMallocCoherent));
     CREATE_TRY(hipHostGetDevicePointer((void**)&e->h_out_dev, e->h_out, 0));
@@ -1327,23 +1332,36 @@ mppi_status mppi_finalize(mppi_engine* e) {
     return finalize_impl(e, true);
 }
 
-// Wait for the finalised step's outputs.  k_finalize writes them into mapped
-// host memory and then, per (vehicle, dim) block, the step's sequence number
-// (after a system-scope fence), so the host sees completion by polling host
-// memory instead of waking on the output event (which also trails the kernel by
-// one queue packet).  The event stays the backstop: it is queried every few
-// hundred polls, which also surfaces a faulted queue as an error.
+// True when every output record of the pending read step carries its sequence number (the
+// tag is each record's last word; k_finalize writes a record with one 16 B store).
+static bool records_tagged(const mppi_engine* e, uint32_t want) {
+    const volatile uint32_t* r = (const volatile uint32_t*)(e->h_out + off_flags(e));
+    const size_t n = rec_count(e);
+    for (size_t i = 0; i < n; ++i)
+        if (r[4 * i + 3] != want) return false;
+    return true;
+}
+
+// One output record, read with one aligned 16 B load (atomic on x86-64 processors with AVX),
+// so its values and its tag come from the same store.  false: the tag is not this step's.
+static inline bool load_record(const mppi_engine* e, size_t i, uint32_t want, uint32_t (&w)[4]) {
+    const __m128i x = _mm_load_si128((const __m128i*)(e->h_out + off_flags(e)) + i);
+    _mm_storeu_si128((__m128i*)w, x);
+    return w[3] == want;
+}
+
+// Wait for the finalised step's outputs.  k_finalize writes them into mapped host memory
+// as tagged records (the step's sequence number in each), so the host sees completion by
+// polling host memory instead of waking on the output event (which also trails the kernel
+// by one queue packet).  The event stays the backstop: it is queried every few hundred
+// polls, which also surfaces a faulted queue as an error.
 static mppi_status wait_outputs(mppi_engine* e) {
     if (e->aql_out) return aql_join(e);   // a native batch: its completion signal (system-scope release)
     if (e->aql_call) {   // a native control call: its flags, the queue's error state as the backstop
-        const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
-        const int n = e->V * e->A;
         const uint32_t want = e->out_seq;
         const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t it = 1;; ++it) {
-            int j = 0;
-            while (j < n && fl[j] == want) ++j;
-            if (j == n) break;
+            if (records_tagged(e, want)) break;
             if ((it & 255u) == 0) {
                 if (const int q = mppi_aql::step_error(e->aql)) return fail(MPPI_ERR_HIP, "native queue error %d", q);
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
@@ -1357,13 +1375,9 @@ static mppi_status wait_outputs(mppi_engine* e) {
         return MPPI_OK;
     }
     if (!e->event_wait) {
-        const volatile uint32_t* fl = (const volatile uint32_t*)(e->h_out + off_flags(e));
-        const int n = e->V * e->A;
         const uint32_t want = e->out_seq;
         for (uint64_t it = 1;; ++it) {
-            int j = 0;
-            while (j < n && fl[j] == want) ++j;
-            if (j == n) {
+            if (records_tagged(e, want)) {
                 std::atomic_thread_fence(std::memory_order_acquire);
                 return MPPI_OK;
             }
@@ -1376,6 +1390,42 @@ static mppi_status wait_outputs(mppi_engine* e) {
         }
     }
     HIP_TRY(hipEventSynchronize(e->ev_out));
+    return MPPI_OK;
+}
+
+// The read step's outputs from its records into host staging in the plain arrays' layout
+// (qdes/vdes or x/v per dim, u0, stats).  The plain arrays are the base (the quadrotor's
+// outputs are formed on the host from u0).
+static mppi_status assemble_records(mppi_engine* e) {
+    const int V = e->V, A = e->A, od = e->out_dim, model = e->cfg.model;
+    const uint32_t want = e->out_seq;
+    e->rec_out.assign((const double*)e->h_out, (const double*)e->h_out + (size_t)V * od);
+    e->rec_u0.resize((size_t)V * A);
+    e->rec_stats.resize((size_t)V * 4);
+    const int qoff = (model == MPPI_MODEL_WHOLEBODY) ? 3 : 0, nq = A - qoff;
+    uint32_t w[4];
+    for (int v = 0; v < V; ++v) {
+        const size_t r0 = (size_t)v * (2 * A + 1);
+        for (int a = 0; a < A; ++a) {
+            double o1, o2;
+            if (!load_record(e, r0 + 2 * a, want, w)) return fail(MPPI_ERR_STATE, "output record (%d,%d) not tagged", v, a);
+            std::memcpy(&o1, w, 8);
+            std::memcpy(&e->rec_u0[(size_t)v * A + a], &w[2], 4);
+            if (!load_record(e, r0 + 2 * a + 1, want, w)) return fail(MPPI_ERR_STATE, "output record (%d,%d) not tagged", v, a);
+            std::memcpy(&o2, w, 8);
+            if (a == 0) std::memcpy(&e->rec_stats[(size_t)v * 4 + 3], &w[2], 4);
+            double* ov = e->rec_out.data() + (size_t)v * od;
+            if (model == MPPI_MODEL_QUADROTOR) continue;
+            if (model == MPPI_MODEL_DRONE || (model == MPPI_MODEL_WHOLEBODY && a < 3)) {
+                ov[a] = o1; ov[3 + a] = o2;
+            } else {
+                const int base = (model == MPPI_MODEL_WHOLEBODY) ? 6 : 0, j = a - qoff;
+                ov[base + j] = o1; ov[base + nq + j] = o2;
+            }
+        }
+        if (!load_record(e, r0 + 2 * A, want, w)) return fail(MPPI_ERR_STATE, "stats record %d not tagged", v);
+        std::memcpy(&e->rec_stats[(size_t)v * 4], w, 12);
+    }
     return MPPI_OK;
 }
 
@@ -1409,6 +1459,13 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
     const double* o = (const double*)e->h_out;
     const float* uu = (const float*)(e->h_out + off_u0(e));
     const float* st = (const float*)(e->h_out + off_stats(e));
+    if (!e->aql_out && e->out_seq != 0u) {   // a read step: its values from its tagged records
+        mppi_status rs = assemble_records(e);
+        if (rs != MPPI_OK) return rs;
+        o = e->rec_out.data();
+        uu = e->rec_u0.data();
+        st = e->rec_stats.data();
+    }
     if (out) std::memcpy(out, o, sizeof(double) * e->V * e->out_dim);
     if (out && e->cfg.model == MPPI_MODEL_QUADROTOR)
         for (int v = 0; v < e->V; ++v)

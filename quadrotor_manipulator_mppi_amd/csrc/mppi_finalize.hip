@@ -348,6 +348,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         u0p[(size_t)v * A + a] = u0;
         double* out = outp + (size_t)v * odim;
         const bool drone_dim = (model == MPPI_MODEL_DRONE) || (model == MPPI_MODEL_WHOLEBODY && a < 3);
+        double o1 = 0.0, o2 = 0.0;   // this dim's two outputs (position, velocity)
         if (model == MPPI_MODEL_QUADROTOR) {
             // coupled dims (thrust rotated by R(rpy)): the host forms the outputs from u0
             // (mppi_capi.cpp quad_outputs)
@@ -355,8 +356,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             const float x0 = x0f, v0 = v0f;
             const float xo = (x0 + v0 * dt) + (0.5f * u0) * dt2;
             const float vo = v0 + dt * u0;
-            out[a] = xo;
-            out[3 + a] = vo;
+            o1 = xo;
+            o2 = vo;
+            out[a] = o1;
+            out[3 + a] = o2;
         } else {           // mppi.py:157-158 (qdes uses the OLD u_prev[0])
             const int j = a - qoff;
             const int base = (model == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
@@ -364,32 +367,38 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             const float t2 = ((0.5f * u0) * dt) * dt;
             const float t3 = u0 * dt;
             if (sf64 && model == MPPI_MODEL_ARM) {
-                out[base + j] = (x0d + (double)t1) + (double)t2;
-                out[base + nq + j] = v0d + (double)t3;
+                o1 = (x0d + (double)t1) + (double)t2;
+                o2 = v0d + (double)t3;
             } else {
-                out[base + j] = (double)((x0f + t1) + t2);
-                out[base + nq + j] = (double)(v0f + t3);
+                o1 = (double)((x0f + t1) + t2);
+                o2 = (double)(v0f + t3);
             }
+            out[base + j] = o1;
+            out[base + nq + j] = o2;
         }
+        const float ess = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
         if (a == 0) {
             float* st = stats + (size_t)v * 4;
             st[0] = rho;
             st[1] = eta;
-            st[2] = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
+            st[2] = ess;
             st[3] = nanf;
         }
-        // completion flag: the outputs above reach host memory first (mppi_capi.cpp wait_outputs).
-        // seq == 0: nobody waits on this step (mppi_run_steps before its last step) -- no
-        // system-scope fence, whose L2 writeback costs ~1.5 us of kernel time.  A read step
-        // needs it although the outputs are in fine-grained (coherent) host memory, and it is
-        // the cheapest correct protocol measured (tests/test_gpu_flag.py stress,
-        // profiles/r03/flag_protocol_stress.txt): waiting only for the plain output stores'
-        // acknowledgment let 3 of 9000 calls read outputs their flag did not cover, and
-        // system-scope output stores (written through, acknowledged from the host) plus that
-        // wait were correct but 2 us slower per control call.
+        // Completion of a read step (seq != 0; mppi_run_steps' earlier steps have none): tagged
+        // output records in mapped host memory, each ONE 16 B store carrying the step's sequence
+        // number beside its values -- (o1, u0, seq) and (o2, nan flag, seq) per dim, (rho, eta,
+        // ess, seq) per vehicle -- so the host takes the values from a record whose own tag it
+        // checks (mppi_capi.cpp wait_outputs / mppi_read_outputs) and nothing needs ordering
+        // against anything else: no system-scope fence (an L2 writeback of ~1.5 us of kernel
+        // time on the call's latency path) and no separate flag store.  The plain arrays above
+        // stay for the native batches (completed by their packet's system-scope release).
         if (seqv != 0u) {
-            __threadfence_system();
-            __hip_atomic_store(flags + (size_t)v * A + a, seqv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4* rec = reinterpret_cast<u32x4*>(flags) + (size_t)v * (2 * A + 1);
+            const uint64_t b1 = (uint64_t)__double_as_longlong(o1), b2 = (uint64_t)__double_as_longlong(o2);
+            rec[2 * a] = u32x4{(uint32_t)b1, (uint32_t)(b1 >> 32), __float_as_uint(u0), seqv};
+            rec[2 * a + 1] = u32x4{(uint32_t)b2, (uint32_t)(b2 >> 32), __float_as_uint(nanf), seqv};
+            if (a == 0) rec[2 * A] = u32x4{__float_as_uint(rho), __float_as_uint(eta), __float_as_uint(ess), seqv};
         }
     }
     FSTAMP(6);
