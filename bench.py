@@ -206,10 +206,15 @@ def cpu_baseline(workload: str, cell_budget_s: float):
     import torch
     n_all = torch.get_num_threads()
     cells = {}
+    # the thread counts: the job's share of the host (torch's pool = OMP_NUM_THREADS, 16 per GPU
+    # on the GPU pool, whose rule is to stay within that share), 1, and a midpoint, so the cells
+    # show how the oracle step scales with threads
+    mid = max(2, n_all // 4) if n_all >= 4 else None
+    counts = [("threads_all", n_all)] + ([(f"threads_{mid}", mid)] if mid and mid != n_all else []) + [("threads_1", 1)]
     for name, (model, K, H) in CPU_SHAPES.items():
         fn = _cpu_step_fn(model, K, H)
         cells[name] = {"model": model, "K": K, "H": H}
-        for tag, nt in (("threads_all", n_all), ("threads_1", 1)):
+        for tag, nt in counts:
             torch.set_num_threads(nt)
             t = _time_cell(fn, cell_budget_s)
             p50, p99 = float(np.median(t)), float(np.percentile(t, 99))
@@ -218,8 +223,14 @@ def cpu_baseline(workload: str, cell_budget_s: float):
             log(f"cpu {name} {tag}={nt}: p50 {p50 * 1e3:.2f} ms p99 {p99 * 1e3:.2f} ms ({t.size} steps)")
         torch.set_num_threads(n_all)
     head = cells[CPU_HEADLINE.get(workload, "c3_arm_k4096_h32")]
+    try:
+        local = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        local = None
     host = {"os_cpu_count": os.cpu_count(), "cpu_model": cpu_model(), "torch_threads": n_all,
-            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "affinity_cpus": local,
+            "note": ("threads_all = torch's pool = the job's CPU share (OMP_NUM_THREADS); the GPU pool asks a job "
+                     "to stay within it, so the affinity set's remaining cores (other GPUs' shares) are not used")}
     hv = head["threads_all"]
     line = {"value": hv["rollout_steps_per_s"], "unit": "rollout-steps/s", "cores": n_all, "kind": "port",
             "p50_ms": hv["p50_ms"], "p99_ms": hv["p99_ms"],

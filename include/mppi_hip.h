@@ -265,9 +265,14 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 
 /* How the last mppi_run_steps and the last mppi_step were dispatched:
- * "<aql | hip: why not native>; calls: <aql | hip>".  One-vehicle control calls with device
- * noise also go out as native packets: the state rides in the rollout's arguments, written
- * into pinned host memory per call. */
+ * "<aql | hip: why not native>; calls: <aql (arguments in <where>) | hip>".  One-vehicle control
+ * calls with device noise also go out as native packets: the state rides in the rollout's
+ * arguments, which the host writes per call into a ring of blocks in host-writable device memory
+ * (the GPU's CPU-visible kernarg or fine-grained pool, through the BAR, followed by an HDP
+ * flush), or into pinned host memory when the device has no such pool or MPPI_AQL_CALL_HOSTMEM=1.
+ * Native dispatch is refused (HIP launches instead, the reason here) when the engine's queue
+ * fails its creation probe: dispatch ids that are not the queue's packet indices, as under a
+ * tool that intercepts queues (rocprofv3 --pmc). */
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len);
 
 mppi_status mppi_synchronize(mppi_engine* e);

@@ -268,10 +268,15 @@ static void queue_error(hsa_status_t status, hsa_queue_t*, void* data) {
     ((Step*)data)->qerr.store((int)status);
 }
 
+static bool probe_dispatch_ids(Step* s, std::string* why);
+
 Step* step_create(int device, std::string* why) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    Device* d = device_for(device);
-    if (!d->ok) { *why = d->why; return nullptr; }
+    Device* d = nullptr;
+    {   // (g_mu only around the device table: the probe below takes it for its symbol lookup)
+        std::lock_guard<std::mutex> lk(g_mu);
+        d = device_for(device);
+        if (!d->ok) { *why = d->why; return nullptr; }
+    }
     Step* s = new Step();
     s->dev = d;
     hsa_status_t st = hsa_queue_create(d->agent, kQueueSize, HSA_QUEUE_TYPE_SINGLE, queue_error, s, UINT32_MAX,
@@ -306,18 +311,29 @@ Step* step_create(int device, std::string* why) {
         delete s;
         return nullptr;
     }
+    if (!probe_dispatch_ids(s, why)) {   // the queue's dispatch ids are not its packet indices
+        if (!step_destroy(s)) *why += " (and the probe's queue did not drain)";
+        return nullptr;
+    }
     return s;
 }
 
-void step_destroy(Step* s) {
-    if (!s) return;
+bool step_destroy(Step* s) {
+    if (!s) return true;
     std::string e;
-    if (s->outstanding) step_wait(s, 60000, &e);
+    if (s->outstanding && step_wait(s, 60000, &e) != 0) {
+        // kernels may still run against the argument blocks (and the engine's buffers): stop the
+        // queue and leak its memory rather than free what the device may still touch
+        hsa_queue_inactivate(s->q);
+        fprintf(stderr, "[mppi aql] queue did not drain at destroy (%s): its buffers are leaked\n", e.c_str());
+        return false;
+    }
     hsa_signal_destroy(s->done);
     hsa_queue_destroy(s->q);
     (void)hipFree(s->d_args);
     if (s->call_vis) hsa_amd_memory_pool_free(s->h_call); else (void)hipHostFree(s->h_call);
     delete s;
+    return true;
 }
 
 bool step_busy(Step* s) { return s && s->outstanding > 0; }
@@ -408,9 +424,13 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 // writeback cost up to ~0.8 us per C3 step, and only a submission's FIRST packet acquires
 // (agent scope: what the host and the HIP stream wrote since the last batch -- argument
 // blocks, state, target), which saves ~0.28 us per C3 step over an acquire on every packet
-// (tools/aql_fence_probe.py).  What stays dirty in the L2s (the costs S, the readback copies
-// of w_eps) is only read after a batch, behind its last finalize's system-scope release, and
-// every line of it is written by the same block, hence the same XCD, at every step.
+// (tools/aql_fence_probe.py).  Nothing a batch writes to device memory stays dirty in an L2
+// either: the values read only after a batch (the costs S, the readback copies of w_eps, the
+// stored noise) are written through at device scope as well (mppi_device.h st_dev / st_dev_run).
+// Plain stores would leave them dirty across the release-free packets, and since which XCD runs
+// a block is not fixed from step to step (MI355X_MICROARCH.md, "Workgroup dispatch, XCD
+// placement"), two L2s could hold dirty copies of one line from different steps, written back in
+// an undefined order (tests/test_gpu_aql.py, the small-K batch readback test).
 // Diagnostics: MPPI_AQL_FENCES = four digits for the packets after the first.
 static int g_fence[4] = {-1, -1, -1, -1};
 static void load_fences() {
@@ -447,6 +467,69 @@ static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l,
                    (kScope[release] << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint32_t setup = 3u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n((uint32_t*)p, (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
+}
+
+// The rollout's Philox step is arg + (dispatch id >> 1) under native dispatch: this holds only
+// while the dispatch id the packet processor hands the waves equals the packet's index in this
+// queue.  A tool that intercepts the queue (rocprofv3 --pmc injects its counter packets, and the
+// packets the application writes are copied to another queue) breaks that silently: steps would
+// repeat or be skipped.  So every new queue first runs two probe packets (k_dispatch_probe writes
+// its dispatch id) and is used only when both ids equal their packet indices; otherwise the
+// engine keeps HIP launches (mppi_dispatch_info says why).
+static bool probe_dispatch_ids(Step* s, std::string* why) {
+    Kern k;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, "k_dispatch_probe", &k, why)) return false;
+    }
+    unsigned long long* d_ids = nullptr;
+    if (hipMalloc(&d_ids, 2 * sizeof(unsigned long long)) != hipSuccess) { *why = "probe buffer"; return false; }
+    // the two packets' argument blocks (one pointer each) in the batch slots' space
+    unsigned long long* args[2] = {d_ids, d_ids + 1};
+    std::vector<unsigned char> h(2 * kArgSlot, 0);
+    memcpy(h.data(), &args[0], 8);
+    memcpy(h.data() + kArgSlot, &args[1], 8);
+    bool ok = hipMemset(d_ids, 0xFF, 2 * sizeof(unsigned long long)) == hipSuccess &&
+              hipMemcpy(s->d_args + kArgSlot, h.data(), h.size(), hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) { (void)hipFree(d_ids); *why = "probe upload"; return false; }
+    mppi::LaunchDesc l{};
+    snprintf(l.symbol, sizeof l.symbol, "k_dispatch_probe");
+    l.grid[0] = l.grid[1] = l.grid[2] = 1;
+    l.block[0] = 64; l.block[1] = l.block[2] = 1;
+    l.arg_bytes = 8;
+    uint64_t idx[2];
+    hsa_signal_add_relaxed(s->done, 1);
+    ++s->outstanding;
+    for (int i = 0; i < 2; ++i) {
+        idx[i] = hsa_queue_load_write_index_relaxed(s->q);
+        put(s->q, k, l, s->d_args + (1 + i) * kArgSlot, i == 1 ? s->done : hsa_signal_t{0}, 2, i == 1 ? 2 : 0);
+    }
+    hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)idx[1]);
+    std::string err;
+    unsigned long long got[2] = {~0ull, ~0ull};
+    if (step_wait(s, 10000, &err) != 0) {   // (buffer leaked: may be in use)
+        char b[160];
+        snprintf(b, sizeof b, " [signal %ld, read index %llu, write index %llu]", (long)hsa_signal_load_relaxed(s->done),
+                 (unsigned long long)hsa_queue_load_read_index_relaxed(s->q),
+                 (unsigned long long)hsa_queue_load_write_index_relaxed(s->q));
+        *why = "dispatch-id probe: " + err + b;
+        return false;
+    }
+    ok = hipMemcpy(got, d_ids, sizeof got, hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d_ids);
+    if (!ok) { *why = "dispatch-id probe readback"; return false; }
+    if (const char* sk = getenv("MPPI_AQL_PROBE_SKEW")) {   // test hook: the refusal path (tests/test_gpu_aql.py)
+        got[0] += (unsigned long long)atoll(sk);
+        got[1] += (unsigned long long)atoll(sk);
+    }
+    if (got[0] != idx[0] || got[1] != idx[1]) {
+        char b[256];
+        snprintf(b, sizeof b, "the queue's dispatch ids (%llu, %llu) are not its packet indices (%llu, %llu): "
+                 "intercepted by a tool", got[0], got[1], (unsigned long long)idx[0], (unsigned long long)idx[1]);
+        *why = b;
+        return false;
+    }
+    return true;
 }
 
 int step_dispatch(Step* s, int n, std::string* err) {

@@ -20,8 +20,12 @@ namespace mppi_aql {
 struct Step;   // one engine's queue, completion signal and device-resident argument blocks
 
 // nullptr (and why) when native dispatch is unavailable on this device ordinal.
+// The queue is probed first (two packets report their dispatch ids): a queue whose dispatch ids
+// are not its packet indices (intercepted by a tool) is refused.
 Step* step_create(int device, std::string* why);
-void step_destroy(Step* s);
+// false: the queue did not drain (60 s); it is inactivated and its memory leaked, and the caller
+// must not free buffers its kernels may still use.
+bool step_destroy(Step* s);
 
 // Make the device-resident argument blocks hold these two launches such that the next
 // rollout dispatched runs step `step`: the rollout's step word (byte offset step_off of its

@@ -805,6 +805,9 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     }
     nb = std::min(nb, groups);
     int iters = (groups + nb - 1) / nb;
+    // a block's cost run (iters * nw * R samples) is staged in LDS for one write-through store
+    // (k_rollout): at most kMaxCostRun floats, more blocks otherwise
+    iters = std::min(iters, std::max(1, kMaxCostRun / (nw * R)));
     nb = (groups + iters - 1) / iters;
     if (c.model == MPPI_MODEL_QUADROTOR) {   // k_rollout_quad: 16 rollouts (4 lanes each) per dynamics
         e->threads = 256;                     // wave; 1 dynamics wave per block up to 1024 blocks, else 4
@@ -1028,6 +1031,14 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
 
 void mppi_destroy(mppi_engine* e) {
     if (!e) return;
+    (void)hipSetDevice(e->cfg.device);
+    // the native queue first: its last batch may still write the buffers freed below (stamps
+    // included).  A queue that does not drain leaves them leaked rather than freed under it.
+    if (e->aql && !mppi_aql::step_destroy(e->aql)) {
+        fprintf(stderr, "[mppi] mppi_destroy: the engine's native queue did not drain; its device buffers are leaked\n");
+        return;
+    }
+    e->aql = nullptr;
     if (e->d_stamps && e->stamp_n) {
         fprintf(stderr, "[mppi stamps] rollout avg cycles per wave over %lld waves:", (long long)e->stamp_n);
         for (size_t i = 1; i < kRollStampOrder.size(); ++i)
@@ -1036,11 +1047,7 @@ void mppi_destroy(mppi_engine* e) {
         for (size_t i = 1; i < kFinStampOrder.size(); ++i)
             fprintf(stderr, " %s=%.0f", kFinStampNames[i], e->fstamp_sum[i] / std::max<int64_t>(1, e->fstamp_n));
         fprintf(stderr, "\n");
-        (void)hipFree(e->d_stamps);
-        (void)hipFree(e->d_fstamps);
     }
-    (void)hipSetDevice(e->cfg.device);
-    if (e->aql) mppi_aql::step_destroy(e->aql);   // waits for its last batch
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto& pr : e->roll_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -1048,7 +1055,7 @@ void mppi_destroy(mppi_engine* e) {
     if (e->comm) rccl().destroy(e->comm);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);

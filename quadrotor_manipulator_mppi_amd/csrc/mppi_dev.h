@@ -11,6 +11,9 @@ constexpr int kMaxA = MPPI_MAX_ACTION;
 constexpr int kMaxJ = MPPI_MAX_JOINTS;
 constexpr int kMaxW = MPPI_MAX_SAVGOL;
 constexpr int kHdr = 4;  // partial record header: rho, eta, eta2, pad
+// k_rollout stages a block's costs (iters x waves x rollouts per wave consecutive samples) in LDS
+// for one write-through store run; create keeps the run within this many floats (16 KB)
+constexpr int kMaxCostRun = 4096;
 
 // One joint of the chain, pre-baked on the host exactly the way the reference
 // builds its tensors (transformation_matrix.py:28-35, 58-95).

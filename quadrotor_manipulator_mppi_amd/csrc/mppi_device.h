@@ -40,6 +40,15 @@ __device__ __forceinline__ T ld_dev(const T* p) {
 }
 constexpr int kAuxDev = 16;   // the same for buffer loads (cache-policy operand: sc1)
 
+// Stores of values read back only after a native batch (the costs S, the readback copies of
+// w_eps, the stored noise): written through at device scope (sc1), so no XCD's L2 keeps a dirty
+// copy.  Plain stores left such lines dirty across a batch's release-free packets, and which XCD
+// runs a block is not fixed from step to step (MI355X_MICROARCH.md, "Workgroup dispatch, XCD
+// placement"): two L2s could hold dirty copies of one line from different steps, and the order of
+// their write-backs would decide what the host reads after the batch.
+__device__ __forceinline__ void st_dev(float* p, float x) {
+    __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // A pointer the compiler keeps in SGPRs (its halves read from the first lane): built from
 // kernel arguments through 64-bit VALU math it can land in VGPRs, and a buffer resource over
 // it then becomes a waterfall loop around every load or store.
@@ -48,6 +57,25 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     const uint64_t a = (uint64_t)p;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return (T*)(((uint64_t)hi << 32) | lo);
+}
+
+// A run of n consecutive floats from LDS (src) to dst[0..n), dst wave-uniform, written through:
+// thread i stores elements 4i..4i+3 as ONE 16 B sc1 buffer store where all four exist and dst + 4i
+// is 16 B aligned (a block's costs are whole 64 B lines at the common shapes: no partial-line
+// writes, which HBM merges slowly), else one 4 B sc1 store per element.
+__device__ __forceinline__ void st_dev_run(float* dst_uniform, const float* src, int n, int i) {
+    const int e = 4 * i;
+    if (e >= n) return;
+    if (e + 4 <= n && ((((uintptr_t)dst_uniform) + 4u * (uint32_t)e) & 15u) == 0u) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(dst_uniform, 0, (int)0x7FFFFFFF, 0x00020000);
+        const float4 x = *reinterpret_cast<const float4*>(src + e);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 w = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, 4 * e, 0, kAuxDev);
+        return;
+    }
+    for (int j = 0; j < 4 && e + j < n; ++j) st_dev(dst_uniform + e + j, src[e + j]);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic

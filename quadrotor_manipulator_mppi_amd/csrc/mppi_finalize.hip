@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     // FINAL: w_eps = N/eta over the window, SavGol, u += w_eps
     const float etaf = (nanf > 0.0f) ? NAN : eta;
     const float w = __fdividef(N, etaf);
-    if (wraw && own) wraw[((size_t)v * H + t) * A + a] = w;
+    if (wraw && own) st_dev(wraw + ((size_t)v * H + t) * A + a, w);   // (readback: written through)
     FSTAMP(4);
     // SavGol with the reference's symmetric pad (svg_filter.py:58: index -i-1 left of 0,
     // 2H-1-i right of H-1; one reflection suffices, create checks H > window/2): w goes to
@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(5);
     const float un = u_old + sm;
     if (own) {
-        if (wsmooth) wsmooth[((size_t)v * H + t) * A + a] = sm;
+        if (wsmooth) st_dev(wsmooth + ((size_t)v * H + t) * A + a, sm);
         // written through at device scope (the next rollout reads it on every XCD), drained at
         // the end: the native dispatch's finalize packets then need no release (mppi_aql.cpp)
         if (!(MPPI_FIN_KO & 32))   // (32: timing knockout, u_prev not written)
@@ -404,6 +404,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(6);
     FSTAMPRT(14);
     if (!(MPPI_FIN_KO & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Native dispatch's check of its one assumption (mppi_aql.cpp step_create): the dispatch id the
+// waves receive is the packet's index in the engine's queue.  A tool that intercepts the queue
+// (a profiler's counter packets) would break it, and with it the rollout's step counter.
+extern "C" __global__ void __launch_bounds__(64) k_dispatch_probe(unsigned long long* out) {
+    if (threadIdx.x == 0) out[0] = mppi_dispatch_id();
 }
 
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only

@@ -647,7 +647,7 @@ template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bo
 __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_arg, const uint32_t k_off,
                                                  const int32_t noise_arg, const int32_t H_arg,
-                                                 const int32_t nthr,
+                                                 const int32_t geo_arg,
                                                  const float* __restrict__ u_prev,
                                                  const JointDev* __restrict__ jtab, const DevParams pk) {
     constexpr int R = 64 / LSEG;
@@ -662,7 +662,10 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     __shared__ VehicleConst vcv;
     const DevParams& p = pk;
     const int v = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;   // block size as a preloaded argument: blockDim would be an implicit-argument s_load
+    // block size and groups per block as one preloaded argument (threads | iters << 16): blockDim
+    // would be an implicit-argument s_load, p.iters a kernel-argument one
+    const int nthr = geo_arg & 0xFFFF, iters = ONEG ? 1 : (geo_arg >> 16);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
     const int32_t noise_mode = noise_arg & 0xFF;
     const uint32_t step_ctr = step_of(step_arg, noise_arg);   // (native dispatch: from the dispatch id)
@@ -708,7 +711,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // the first group's standard normals overlap the loads above
     float z0[NCH][NA];
     if (noise_mode != MPPI_NOISE_INJECTED) {
-        const uint32_t kg = k_off + (uint32_t)((blockIdx.x * nw + wid) * R + sub);
+        const uint32_t kg = k_off + (uint32_t)((blockIdx.x * iters * nw + wid) * R + sub);   // group 0's k
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
             draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, step_ctr, seed_lo, seed_hi);
@@ -746,6 +749,9 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     const int H = H_arg, K = pk.K;
     constexpr int kWs = wave_slot_floats<NA, NCH, LSEG>();
     float* const xw = smem + ((HA + 3) & ~3) + wid * kWs;   // this wave's LDS slot
+    // the block's costs, all groups (iters * nw * R consecutive k), staged for one write-through
+    // store run after the combine barrier (st_dev_run)
+    float* const s_stage = smem + ((HA + 3) & ~3) + 8 * kWs;
     STAMP(1);
 
     // trajectory planes of vehicle v (from kernel arguments and blockIdx only, so the
@@ -769,7 +775,8 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
     auto group = [&](const int it) __attribute__((always_inline)) {   // (the NCH = 4 extended kernel called it out of line: a 1.7 KB stack frame)
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
-        const int g = blockIdx.x + it * p.nb;
+        // a block's groups are consecutive: its costs form one run of iters * nw * R samples
+        const int g = blockIdx.x * iters + it;
         const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
         const int kc = kval ? k : K - 1;   // clamped: every load stays in bounds
@@ -818,10 +825,10 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
                 eps[c][a] = val ? eps[c][a] : 0.0f;
                 act[c][a] = val ? ur[a] + eps[c][a] : 0.0f;
             }
-            if (p.store_noise && val) {
+            if (p.store_noise && val) {   // (readback only: written through, st_dev)
                 float* dst = p.noise_out + (((size_t)v * K + k) * H + t) * NA;
 #pragma unroll
-                for (int a = 0; a < NA; ++a) dst[a] = eps[c][a];
+                for (int a = 0; a < NA; ++a) st_dev(dst + a, eps[c][a]);
             }
         }
         // extra CostManager terms on the controls (cost_manager.py:83,86): covar
@@ -1099,7 +1106,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         float S_mine = S_seg[0];
 #pragma unroll
         for (int s = 1; s < R; ++s) S_mine = (sub == s) ? S_seg[s] : S_mine;
-        if (kval && t0 == 0) p.S[(size_t)v * K + k] = S_mine;
+        if (kval && t0 == 0) s_stage[(it * nw + wid) * R + sub] = S_mine;
 
         // ---- online softmin (mppi.py:184-188) over this wave's rollouts (scalar bookkeeping)
         float m = INFINITY;
@@ -1144,15 +1151,15 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         if (MPPI_PRIO) set_wave_prio(3);
         group(0);
         if (MPPI_PRIO) set_wave_prio(0);
-    } else if (p.iters == 1) {
+    } else if (iters == 1) {
         group(0);
     } else {
         // Wave priority by remaining groups: the SIMD arbiter otherwise favours the oldest
         // wave, so the waves of a SIMD finish their (equal) work one after another and the
         // last ones run alone, without latency hiding (the grid's tail).  A
         // wave that is ahead drops its priority, the laggards catch up.
-        for (int it = 0; it < p.iters; ++it) {
-            if (MPPI_PRIO) set_wave_prio(p.iters - 1 - it);
+        for (int it = 0; it < iters; ++it) {
+            if (MPPI_PRIO) set_wave_prio(iters - 1 - it);
             group(it);
         }
         if (MPPI_PRIO) set_wave_prio(0);
@@ -1178,6 +1185,12 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     STAMPW(11);
     lds_barrier();
     STAMP(6);
+    {   // the block's costs: one write-through run (st_dev_run), 64 B per block at C3
+        const int nS = iters * nw * R, k0 = blockIdx.x * nS;
+        const int n = min(nS, K - k0);
+        float* const Sv = uniform_ptr(p.S + (size_t)v * K + k0);
+        for (int i = tid; 4 * i < n; i += nthr) st_dev_run(Sv, s_stage, n, i);
+    }
     // rho_b = the min of the 8 wave slots, which every thread reads for f_w anyway (an LDS
     // atomicMin before the barrier cost a waterfall loop and a ds_min per wave)
     float rws[8], rho_b = INFINITY;
@@ -1246,15 +1259,20 @@ inline void rollout_symbol(char* buf, size_t n) {
 
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
 inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
-    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>()) * sizeof(float);
+    const int iters = ONEG ? 1 : p.iters;
+    // (LDS: warm start, 8 wave slots, the block's cost run of iters * 8 * R floats)
+    const int s_run = (iters * 8 * (64 / LSEG) + 3) & ~3;
+    if (threads <= 0 || threads > 512 || iters < 1 || iters * (threads / 64) * (64 / LSEG) > kMaxCostRun) return -1;
+    const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>() + s_run) * sizeof(float);
+    const int32_t geo = threads | (iters << 16);
     if (p.V == 1)
         return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>,
                   rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
-                  p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads, p.u_prev,
+                  p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev,
                   p.joints, p);
     return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>,
               rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
-              p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, threads, p.u_prev, p.joints,
+              p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev, p.joints,
               p);
 }
 

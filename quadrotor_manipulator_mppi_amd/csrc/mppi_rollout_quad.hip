@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
                                                // phase's lane = t reads are bank-conflict free)
     extern __shared__ __attribute__((aligned(16))) float qlds[];   // eps tile [H+1][kQPitch], u_prev [H+1][4]
     __shared__ float e_lds[QR];
+    __shared__ __attribute__((aligned(16))) float s_lds[QR];   // the costs, staged for st_dev_run
     __shared__ float wred[kQWaves][4];         // NWD > 1: the waves' (rho, eta, eta2, nan)
     __shared__ float4 part[kQWaves][64];       // NWD > 1: the waves' record partials (lane = t)
     const DevParams& p = pk;
@@ -154,9 +155,11 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
         float* dst = eps_t + t * kQPitch + r * kQA;
 #pragma unroll
         for (int a = 0; a < kQA; ++a) dst[a] = eps[a];
-        if (p.store_noise && kval)
-            *reinterpret_cast<float4*>(p.noise_out + (((size_t)v * K + k) * H + t) * kQA) =
-                make_float4(eps[0], eps[1], eps[2], eps[3]);
+        if (p.store_noise && kval) {   // (readback only: written through, st_dev)
+            float* dst = p.noise_out + (((size_t)v * K + k) * H + t) * kQA;
+#pragma unroll
+            for (int a = 0; a < kQA; ++a) st_dev(dst + a, eps[a]);
+        }
     }
     if (tid < H * kQA) u_t[tid] = u_r;
     __syncthreads();
@@ -263,7 +266,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     stage = qbc<0>(stage) + qbc<1>(stage) + qbc<2>(stage);
     term = qbc<0>(term) + qbc<1>(term) + qbc<2>(term);
     const float S = kval ? (swsp * stage) + (swtp * term) : INFINITY;
-    if (kval && j == 0) p.S[(size_t)v * K + k] = S;
+    if (j == 0) s_lds[r] = S;
     // ---- online softmin over the block's rollouts (mppi.py:184-188 / drone_mppi.py:111-130)
     const bool mine = kval && j == 0, bad = S != S;
     float rho = wave_fold_all((mine && !bad) ? S : INFINITY, OpMin());
@@ -278,6 +281,10 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     float eta = wave_fold_all(e, OpAdd()), eta2 = wave_fold_all(e * e, OpAdd());
     if (j == 0) e_lds[r] = e;
     wave_lds_handoff();
+    {   // this wave's 16 costs as one write-through 64 B run (mppi_device.h st_dev_run)
+        const int k0 = kb + wid * kQR, n = min(kQR, K - k0);
+        if (lane < 4) st_dev_run(uniform_ptr(p.S + (size_t)v * K + k0), s_lds + wid * kQR, n, lane);
+    }
     // ---- record N[a][t] = sum_k e_k eps_k[t][a], lane = t (each wave its own 16 rollouts)
     float n[kQA] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (lane < H) {

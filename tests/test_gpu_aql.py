@@ -202,3 +202,56 @@ def test_native_control_calls_match_hip(monkeypatch, model, kw):
     assert h.dispatch_info().endswith("calls: hip"), h.dispatch_info()
     h.close()
     a.close()
+
+
+@pytest.mark.parametrize("model,kw", [("arm", dict(n_samples=256, n_horizon=32)),
+                                      ("quadrotor", dict(n_samples=256, n_horizon=32))],
+                         ids=["arm-256-32", "quadrotor-256-32"])
+def test_native_batch_readbacks_written_through(monkeypatch, model, kw):
+    """The values read only after a native batch -- costs S, the readback copies of w_eps, the
+    stored noise -- are written through at device scope (mppi_device.h st_dev / st_dev_run).  At
+    a shape whose working set stays in the L2s (K=256, no trajectory), plain stores would leave
+    their lines dirty across the batch's release-free packets in whichever XCD ran the writing
+    block at each step, and which XCD runs a block is not fixed (MI355X_MICROARCH.md, workgroup
+    placement): the readbacks after a 500-step batch must equal HIP's bit for bit."""
+    h, a = _pair(monkeypatch, model, store_trajectory=False, store_noise=True, **kw)
+    for rnd in range(3):
+        for e in (h, a):
+            e.run_steps(500)
+        _same(h, a, f"500-step batch {rnd}")
+        np.testing.assert_array_equal(a.get_weights(), h.get_weights(), err_msg="weights")
+        ra, sa = a.get_weighted_noise()
+        rh, sh = h.get_weighted_noise()
+        np.testing.assert_array_equal(ra, rh, err_msg="w_eps raw")
+        np.testing.assert_array_equal(sa, sh, err_msg="w_eps smoothed")
+        np.testing.assert_array_equal(a.get_noise(), h.get_noise(), err_msg="stored noise")
+        w = a.get_weights()[0].astype(np.float64)
+        assert abs(w.sum() - 1.0) < 1e-4
+    h.close()
+    a.close()
+
+
+def test_native_dispatch_refused_when_ids_are_not_packet_indices(monkeypatch):
+    """The queue's creation probe (mppi_aql.cpp probe_dispatch_ids): when the dispatch ids the
+    waves receive are not the queue's packet indices (a tool intercepting the queue; simulated
+    here by skewing the probe's readback), the Philox step could not be derived from them, so
+    the engine refuses native dispatch, says why, and the HIP path computes the same steps."""
+    monkeypatch.delenv("MPPI_DISPATCH", raising=False)
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    ref = Engine(make_config("arm", device=0, seed=11, n_samples=1024, n_horizon=32))
+    monkeypatch.setenv("MPPI_AQL_PROBE_SKEW", "6")
+    e = Engine(make_config("arm", device=0, seed=11, n_samples=1024, n_horizon=32))
+    for x in (ref, e):
+        x.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+        x.set_state(_state("arm"))
+        x.run_steps(4)
+        x.synchronize()
+    assert "intercepted" in e.dispatch_info(), e.dispatch_info()
+    assert ref.dispatch_info().startswith("aql;"), ref.dispatch_info()
+    np.testing.assert_array_equal(e.get_u_prev(), ref.get_u_prev())
+    oe, ue, _ = e.step(_state("arm", shift=0.01))
+    orf, ur, _ = ref.step(_state("arm", shift=0.01))
+    np.testing.assert_array_equal(oe, orf)
+    assert e.dispatch_info().endswith("calls: hip"), e.dispatch_info()
+    e.close()
+    ref.close()

@@ -76,7 +76,7 @@ def main():
         for li, path in enumerate(libs):
             a = np.array(res[li, ri])
             q = np.percentile(a, [25, 50, 75], axis=0)
-            print(f"  {os.path.basename(path):18s} step {q[1, 0]:7.2f} [{q[0, 0]:6.2f},{q[2, 0]:6.2f}] us   "
+            print(f"  {os.path.relpath(path):26s} step {q[1, 0]:7.2f} [{q[0, 0]:6.2f},{q[2, 0]:6.2f}] us   "
                   f"call {q[1, 1]:6.2f} [{q[0, 1]:6.2f},{q[2, 1]:6.2f}] us   ({eng[li, ri].dispatch_info()})", flush=True)
     for e in eng.values():
         e.close()
