@@ -265,7 +265,9 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 
 /* How the last mppi_run_steps and the last mppi_step were dispatched:
- * "<aql | hip: why not native>; calls: <aql (arguments in <where>) | hip>".  One-vehicle control
+ * "<aql | hip: why not native>; calls: <aql (arguments in <where>) | hip>; step: <fused | fused
+ * rollout+pack | two kernels: why>" -- fused: one k_rollout launch per step whose last-arriving blocks
+ * fold the records and finalise (or pack a shard's slot) in the same launch.  One-vehicle control
  * calls with device noise also go out as native packets: the state rides in the rollout's
  * arguments, which the host writes per call into a ring of blocks in host-writable device memory
  * (the GPU's CPU-visible kernarg or fine-grained pool, through the BAR, followed by an HDP

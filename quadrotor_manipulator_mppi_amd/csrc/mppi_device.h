@@ -25,7 +25,10 @@ namespace {
 // relative to the dispatch id -- step = arg + (dispatch id >> 1) -- so one argument block,
 // written once, serves every (rollout, finalize) pair the engine's queue runs
 constexpr int32_t kNoiseStepFromId = 0x100;
+// the same for a queue of single-packet steps (the fused step: step = arg + dispatch id)
+constexpr int32_t kNoiseStepFromId1 = 0x200;
 __device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg) {
+    if (noise_arg & kNoiseStepFromId1) return step_arg + (uint32_t)mppi_dispatch_id();
     return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
 }
 
@@ -58,6 +61,19 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return (T*)(((uint64_t)hi << 32) | lo);
 }
+
+// Block-uniform values into SGPRs (v_readfirstlane; free when the value is scalar already).  In
+// a kernel that stores to global memory the compiler cannot load its parameter blocks with
+// scalar loads (fin_body inside the fused rollout), and an "s" asm operand fed by a vector load
+// is an illegal VGPR-to-SGPR copy.
+__device__ __forceinline__ int32_t rfl(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ int64_t rfl(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <typename T>
+__device__ __forceinline__ T* rfl(T* p) { return uniform_ptr(p); }
 
 // A run of n consecutive floats from LDS (src) to dst[0..n), dst wave-uniform, written through:
 // thread i stores elements 4i..4i+3 as ONE 16 B sc1 buffer store where all four exist and dst + 4i

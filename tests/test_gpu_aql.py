@@ -199,7 +199,7 @@ def test_native_control_calls_match_hip(monkeypatch, model, kw):
             np.testing.assert_array_equal(oa2, oa)
             np.testing.assert_array_equal(ua2, ua)
     assert "calls: aql" in a.dispatch_info(), a.dispatch_info()
-    assert h.dispatch_info().endswith("calls: hip"), h.dispatch_info()
+    assert "calls: hip;" in h.dispatch_info(), h.dispatch_info()
     h.close()
     a.close()
 
@@ -252,6 +252,6 @@ def test_native_dispatch_refused_when_ids_are_not_packet_indices(monkeypatch):
     oe, ue, _ = e.step(_state("arm", shift=0.01))
     orf, ur, _ = ref.step(_state("arm", shift=0.01))
     np.testing.assert_array_equal(oe, orf)
-    assert e.dispatch_info().endswith("calls: hip"), e.dispatch_info()
+    assert "calls: hip;" in e.dispatch_info(), e.dispatch_info()
     e.close()
     ref.close()

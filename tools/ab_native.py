@@ -1,6 +1,9 @@
 """Interleaved same-process A/B of library builds on the NATIVE dispatch path (tools/, not shipped).
 
-    python tools/ab_native.py <reps> "<model K H [V]>;..." lib_a.so lib_b.so ...
+    python tools/ab_native.py <reps> "<model K H [V]>;..." lib_a.so lib_b.so[@VAR=value,...] ...
+
+A build may carry environment settings read at engine creation (lib.so@MPPI_FUSED=0): they are
+set while that build's engines are created.
 
 Each build is loaded into the one process (RTLD_LOCAL; its code objects next to it), one engine
 per (build, workload); per rep and build: a 50-step priming batch, then the wall time of a
@@ -38,7 +41,11 @@ def main():
     steps = int(os.environ.get("MPPI_AB_STEPS", "500"))
     ncalls = int(os.environ.get("MPPI_AB_CALLS", "20"))   # 0 for builds without completion flags (knockouts)
     eng = {}
-    for li, p in enumerate(libs):
+    for li, spec in enumerate(libs):
+        p, _, envs = spec.partition("@")
+        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         capi._lib = load(p)
         for ri, r in enumerate(runs):
             model, K, H = r[0], int(r[1]), int(r[2])
@@ -53,6 +60,11 @@ def main():
             e.run_steps(20)
             e.synchronize()
             eng[li, ri] = e
+        for k, val in saved.items():
+            if val is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = val
     res = {k: [] for k in eng}
     for rep in range(reps):
         for ri, r in enumerate(runs):
