@@ -265,9 +265,7 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 
 /* How the last mppi_run_steps and the last mppi_step were dispatched:
- * "<aql | hip: why not native>; calls: <aql (arguments in <where>) | hip>; step: <fused | fused
- * rollout+pack | two kernels: why>" -- fused: one k_rollout launch per step whose last-arriving blocks
- * fold the records and finalise (or pack a shard's slot) in the same launch.  One-vehicle control
+ * "<aql | hip: why not native>; calls: <aql (arguments in <where>) | hip>".  One-vehicle control
  * calls with device noise also go out as native packets: the state rides in the rollout's
  * arguments, which the host writes per call into a ring of blocks in host-writable device memory
  * (the GPU's CPU-visible kernarg or fine-grained pool, through the BAR, followed by an HDP
@@ -286,7 +284,9 @@ mppi_status mppi_synchronize(mppi_engine* e);
  *   traj     (V,K,H,C) C = traj_channels    DRONE p(3) / ARM q(nq)+EE(16) / WB p(3)+q(nq)+EE(16)
  *                                            QUADROTOR xyz(3)+rpy(3) (drone_mppi.py:62 trajectory)
  *            EE as the 4x4 row-major matrix of urdf_fk.py:108       [store_trajectory]
- *   wnoise   w_eps before / after SavGol (V,H,A)                     */
+ *   wnoise   w_eps before / after SavGol (V,H,A), recomputed from the records the last
+ *            step combined (a k_finalize launch in READBACK mode): the step itself stores
+ *            no readback copies                                      */
 mppi_status mppi_get_costs(mppi_engine* e, float* S);
 mppi_status mppi_get_weights(mppi_engine* e, float* w);
 mppi_status mppi_get_noise(mppi_engine* e, float* eps);
@@ -301,8 +301,9 @@ mppi_status mppi_get_timing(mppi_engine* e, double* rollout_ms_total, double* fi
  * bracketed by one event pair, then n finalize launches bracketed by another (the
  * per-launch pairs of mppi_enable_timing add ~2-3 us of event overhead each).  The
  * warm start and step counter are saved and restored, and the timing launches write
- * their outputs (out/u0/stats, weighted noise) to device scratch, so the controller
- * state and a pending mppi_read_outputs / mppi_get_weighted_noise are unchanged.  The
+ * their outputs (out/u0/stats) to device scratch, so the controller state and a pending
+ * mppi_read_outputs are unchanged (mppi_get_weighted_noise then reflects the timing launches'
+ * records: read it before timing).  The
  * trajectory and cost buffers (mppi_get_trajectory / mppi_get_costs / mppi_get_weights)
  * DO hold the timing loop's last rollout afterwards.  Single-shard engines with device
  * noise. */

@@ -34,7 +34,7 @@ _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
 SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
            ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=14"]),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
-HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_finbody.h", "mppi_aql.h",
+HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",
            os.path.join("..", "..", "include", "mppi_hip.h")]
 # Native dispatch (mppi_aql.cpp) loads each kernel unit's gfx950 code object from next to the
 # library: <library stem>.<unit>.co, built from the same source with the same flags.

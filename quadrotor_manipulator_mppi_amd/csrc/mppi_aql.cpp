@@ -257,7 +257,6 @@ struct Step {
     bool call_unread = false;             // the last call's outputs not yet seen (step_call_read)
     mppi::LaunchDesc roll{}, fin{};       // what the device blocks hold (step word as uploaded)
     Kern kr, kf;
-    int pps = 2;                          // packets per step: 2 (rollout, finalize) or 1 (fused step)
     uint32_t step_off = 0, step_word = 0; // the resident rollout's dispatch-id relative step word
     bool valid = false;
     int64_t outstanding = 0;              // batches dispatched and not yet waited for
@@ -270,7 +269,6 @@ static void queue_error(hsa_status_t status, hsa_queue_t*, void* data) {
 }
 
 static bool probe_dispatch_ids(Step* s, std::string* why);
-static void put_barrier(hsa_queue_t* q);
 
 Step* step_create(int device, std::string* why) {
     Device* d = nullptr;
@@ -367,22 +365,13 @@ static bool same_launch(const mppi::LaunchDesc& a, const mppi::LaunchDesc& b, ui
 
 static unsigned char* batch_args(Step* s) { return s->d_args + (1 + 2 * (size_t)s->batch_slot) * kArgSlot; }
 
-int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* finp, uint32_t step,
+int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
                  uint32_t step_off, std::string* err) {
-    // the next rollout's packet index: the queue holds (rollout, finalize) pairs only -- rollouts
-    // at indices of one parity, (index >> 1) counts pairs -- or fused single-packet steps only
-    // (the index counts steps); a batch of the other kind is dispatched after a wait (below)
-    const int pps = finp ? 2 : 1;
-    const mppi::LaunchDesc& fin = finp ? *finp : roll;
-    const uint64_t wi = hsa_queue_load_write_index_relaxed(s->q);
-    if (s->outstanding && pps != s->pps && step_wait(s, 60000, err) != 0) return -1;
-    if (pps == 2 && (wi & 1)) {   // a pair must start at an even index: pad with a no-op barrier packet
-        put_barrier(s->q);
-        return step_prepare(s, roll, finp, step, step_off, err);
-    }
-    const uint32_t word = step - (uint32_t)(pps == 2 ? wi >> 1 : wi);
-    if (s->valid && s->pps == pps && s->step_word == word && s->step_off == step_off &&
-        same_launch(roll, s->roll, step_off) && (pps == 1 || same_launch(fin, s->fin, ~0u)))
+    // the next rollout's packet index (the queue holds (rollout, finalize) pairs only, so
+    // rollouts sit at indices of one parity and (index >> 1) counts pairs)
+    const uint32_t word = step - (uint32_t)(hsa_queue_load_write_index_relaxed(s->q) >> 1);
+    if (s->valid && s->step_word == word && s->step_off == step_off && same_launch(roll, s->roll, step_off) &&
+        same_launch(fin, s->fin, ~0u))
         return 0;
     if (getenv("MPPI_AQL_PROFILE") && s->valid) {   // diagnostics: why the blocks are re-uploaded
         int first = -1;
@@ -401,7 +390,6 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* 
     }
     if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
     if (step_off + 4 > roll.arg_bytes) { *err = "step counter outside the rollout's arguments"; return -2; }
-    s->pps = pps;
     // the queue may still be reading the blocks about to be overwritten
     if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
     std::vector<unsigned char> h(2 * kArgSlot, 0);
@@ -481,19 +469,6 @@ static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l,
     __atomic_store_n((uint32_t*)p, (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
 }
 
-// A no-op barrier-AND packet (no dependencies): advances the queue by one index, so a batch or
-// call of (rollout, finalize) pairs starts at an even packet index after fused single-packet steps.
-static void put_barrier(hsa_queue_t* q) {
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
-    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
-    auto* p = (hsa_barrier_and_packet_t*)q->base_address + (idx & (q->size - 1));
-    memset((char*)p + 4, 0, sizeof(*p) - 4);
-    const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                                       (1 << HSA_PACKET_HEADER_BARRIER));
-    __atomic_store_n((uint32_t*)p, (uint32_t)header, __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
-}
-
 // The rollout's Philox step is arg + (dispatch id >> 1) under native dispatch: this holds only
 // while the dispatch id the packet processor hands the waves equals the packet's index in this
 // queue.  A tool that intercepts the queue (rocprofv3 --pmc injects its counter packets, and the
@@ -569,23 +544,16 @@ int step_dispatch(Step* s, int n, std::string* err) {
     load_fences();
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
-        if (s->pps == 1) {   // the fused step: one packet
-            put(s->q, s->kr, s->roll, ra, last ? s->done : none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0],
-                last ? 2 : g_fence[1]);
-        } else {
-            put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
-            put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
-        }
+        put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
+        put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
         // the doorbell takes the index of the last packet written
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     }
     return 0;
 }
 
-int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* finp, uint32_t step,
+int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
               uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err) {
-    const int pps = finp ? 2 : 1;
-    const mppi::LaunchDesc& fin = finp ? *finp : roll;
     if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
     static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: phases of a call
     static double pacc[4] = {0, 0, 0, 0};
@@ -603,10 +571,7 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* fin
     // engine reads every call's outputs before the next call (its flag: that rollout has run),
     // so only an unread call waits; a queued batch does not read this block.
     if (s->call_unread && s->outstanding && step_wait(s, 60000, err) != 0) return -1;
-    if (s->outstanding && pps != s->pps && step_wait(s, 60000, err) != 0) return -1;
-    s->pps = pps;
-    if (pps == 2 && (hsa_queue_load_write_index_relaxed(s->q) & 1)) put_barrier(s->q);   // pairs at even indices
-    if (pps == 2 && (!s->call_valid || !same_launch(fin, s->fin_call, ~0u))) {
+    if (!s->call_valid || !same_launch(fin, s->fin_call, ~0u)) {
         if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
         std::vector<unsigned char> h(kArgSlot, 0);
         memcpy(h.data(), fin.args, fin.arg_bytes);
@@ -621,8 +586,8 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* fin
     s->kc_r = kr;
     s->kc_f = kf;
     const uint64_t r = hsa_queue_load_write_index_relaxed(s->q);   // this call's rollout packet
-    const uint32_t word = step - (uint32_t)(pps == 2 ? r >> 1 : r);
-    *seq = 0x80000000u | (uint32_t)(r & 0x7FFFFFFFu);   // the packet index: unique per call in either mode
+    const uint32_t word = step - (uint32_t)(r >> 1);
+    *seq = 0x80000000u | (uint32_t)(r >> 1);
     const uint32_t slot = s->call_slot++ % kCallSlots;
     unsigned char* blk = s->h_call + (size_t)slot * kArgSlot;
     alignas(16) unsigned char tmp[kArgSlot];
@@ -650,12 +615,8 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* fin
     s->call_unread = true;
     const hsa_signal_t none{0};
     load_fences();
-    if (pps == 1) {
-        put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, s->done, std::max(1, g_fence[0]), 2);
-    } else {
-        put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
-        put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
-    }
+    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
+    put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
     hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     if (prof) {
         const auto p4 = now();

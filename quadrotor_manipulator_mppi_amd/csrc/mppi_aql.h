@@ -27,15 +27,14 @@ Step* step_create(int device, std::string* why);
 // must not free buffers its kernels may still use.
 bool step_destroy(Step* s);
 
-// Make the device-resident argument blocks hold these two launches (fin == nullptr: the fused
-// step, one packet per step) such that the next rollout dispatched runs step `step`: the
-// rollout's step word (byte offset step_off of its arguments, dispatch-id relative) becomes
-// step - (next packet index >> 1), or step - next packet index for single-packet steps.  Uploads only when
+// Make the device-resident argument blocks hold these two launches such that the next
+// rollout dispatched runs step `step`: the rollout's step word (byte offset step_off of its
+// arguments, dispatch-id relative) becomes step - (next packet index >> 1).  Uploads only when
 // a launch differs from the resident one (the step word excluded) or the resident step word
 // would not give `step`; waits for the queue to drain before overwriting.  0; -2 when the launches
 // cannot be dispatched natively (a symbol the code objects lack, hidden arguments);
 // -1 on a runtime failure (*err says why).
-int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* fin, uint32_t step,
+int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
                  uint32_t step_off, std::string* err);
 // n (rollout, finalize) pairs, each kernel dependent on the one before; the last finalize
 // carries the completion signal and a system-scope release.
@@ -46,7 +45,7 @@ int step_dispatch(Step* s, int n, std::string* err);
 // writes `seq` into the rollout's arguments at seq_off (the vehicle constants' spare word,
 // which the rollout hands to the finalize) and polls the completion flags for it: bit 31 set,
 // unique per call.  0 / -2 / -1 as step_prepare.
-int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc* fin, uint32_t step,
+int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
               uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err);
 // The last call's outputs have been seen (its completion flags): its rollout has run.
 void step_call_read(Step* s);

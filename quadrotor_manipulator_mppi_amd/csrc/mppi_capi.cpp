@@ -346,12 +346,6 @@ struct mppi_engine {
     int fin_ts = 1, fin_tsz = 8;   // finalize t-slices
     unsigned char* d_out = nullptr;   // device scratch in h_out's layout (mppi_kernel_timing's outputs)
     FinTail* d_tail = nullptr;        // [kTailSlots] the finalize's tail parameters per launch kind
-    // the fused step (k_rollout FUSE): the rollout's last-arriving blocks run the
-    // finalize (FINAL) or the shard's PACK in the same launch -- one kernel per step
-    bool fuse = false;                 // this engine's steps are fused (mppi_fusable; MPPI_FUSED=0: never)
-    std::string fuse_why;              // why not
-    FusedFin* d_ff = nullptr;          // [kTailSlots] per launch kind, as d_tail
-    unsigned long long* d_cnt = nullptr;   // (V) arrival counters
     float* d_wraw = nullptr;
     float* d_wsmooth = nullptr;
     float* d_w = nullptr;
@@ -411,30 +405,6 @@ FinTail tail_of(const FinParams& f, int32_t mode) {
     std::memcpy(t.sg, f.sg, sizeof(t.sg));
     return t;
 }
-
-// Why this engine's steps cannot be fused (nullptr: they can).  The FUSE instantiations of
-// k_rollout exist for the common kernel (diagonal Sigma, no extra cost terms, the Kinova chain or
-// the drone) with one 64-lane chunk per rollout (H <= 64) and 512-thread blocks; the fused tail
-// runs fin_body with CW = 16 (a t-slice of 8 plus the SavGol halo: window 5 or 9) and needs at
-// least as many rollout blocks as folding blocks (A x t-slices, at most 256: they poll beside the
-// rest of the grid, so they must fit on the chip with it).
-constexpr bool kFuseDefault = false;   // the engines' default (MPPI_FUSED unset)
-const char* fuse_ineligible(const mppi_engine* e) {
-    const char* env = getenv("MPPI_FUSED");   // 1: fuse where eligible, 0: never; unset: kFuseDefault
-    if (env ? !strcmp(env, "0") : !kFuseDefault) return "MPPI_FUSED=0";
-    const mppi_config& c = e->cfg;
-    const DevParams& p = e->dp;
-    if (c.model == MPPI_MODEL_QUADROTOR) return "quadrotor model (k_rollout_quad)";
-    if (e->threads != 512) return "block_threads != 512";
-    if (p.nch != 1) return "H > 64";
-    if (c.cost_terms || !p.sigma_diag || (c.model != MPPI_MODEL_DRONE && p.chain_fast != 2))
-        return "extended kernel (cost terms, full Sigma or a generic chain)";
-    if (c.savgol_window != 5 && c.savgol_window != 9) return "SavGol window other than 5 or 9";
-    if (e->A * e->fin_ts > std::min(p.nb, 256)) return "fewer rollout blocks than folding blocks";
-    return nullptr;
-}
-
-void block_records(const mppi_engine* e, FinParams& f);
 
 // a shard's PACK fields (mppi_rollout) into FinParams, and into the PACK tail copy
 void pack_fields(const mppi_engine* e, FinParams& f) {
@@ -1046,6 +1016,11 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
         t[kTailScratch].flags = (uint32_t*)(e->d_out + off_flags(e));
         t[kTailScratch].wraw = nullptr;
         t[kTailScratch].wsmooth = nullptr;
+        // the step's FINAL stores no readback copies of w_eps: mppi_get_weighted_noise recomputes
+        // them from the last step's records (READBACK), so the step's tail carries no extra stores
+        t[kTailFinal].wraw = nullptr;
+        t[kTailFinal].wsmooth = nullptr;
+        t[kTailReadback] = tail_of(f, 2);
         hipError_t te = hipMalloc(&e->d_tail, sizeof(t));
         if (te == hipSuccess) te = hipMemcpy(e->d_tail, t, sizeof(t), hipMemcpyHostToDevice);
         if (te != hipSuccess) {
@@ -1054,36 +1029,6 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
             return MPPI_ERR_HIP;
         }
         f.tail = e->d_tail + kTailFinal;
-    }
-    if (const char* why = fuse_ineligible(e)) {
-        e->fuse_why = why;
-    } else {   // the fused step's launch descriptions (one per tail kind) and arrival counters
-        FusedFin ff[kTailSlots];
-        const size_t nfs = (size_t)e->V * e->A * e->fin_ts * kStamps;
-        for (int k = 0; k < kTailSlots; ++k) {
-            FusedFin& x = ff[k];
-            std::memset(&x, 0, sizeof(x));
-            FinParams r = f;
-            block_records(e, r);
-            x.hdr = r.hdr; x.dat = r.dat; x.tail = e->d_tail + k;
-            x.nrec_H = (uint32_t)r.nrec | ((uint32_t)H << 16);
-            x.geo = (uint32_t)f.tsz | ((uint32_t)f.half << 8) | ((uint32_t)f.ts << 16) | ((uint32_t)e->A << 24);
-            x.hdr_rs = (int32_t)r.hdr_rs; x.d_rs = (int32_t)r.d_rs; x.d_as = (int32_t)r.d_as;
-            x.hdr_vs = (int32_t)r.hdr_vs; x.d_vs = (int32_t)r.d_vs;
-            x.nfold = e->A * f.ts; x.nt = 512; x.win = c.savgol_window;
-            x.stamps = e->d_fstamps ? e->d_fstamps + (k == kTailPack ? nfs : 0) : nullptr;
-        }
-        hipError_t te = hipMalloc(&e->d_cnt, sizeof(unsigned long long) * e->V);
-        if (te == hipSuccess) te = hipMemset(e->d_cnt, 0, sizeof(unsigned long long) * e->V);
-        for (auto& x : ff) x.cnt = e->d_cnt;
-        if (te == hipSuccess) te = hipMalloc(&e->d_ff, sizeof(ff));
-        if (te == hipSuccess) te = hipMemcpy(e->d_ff, ff, sizeof(ff), hipMemcpyHostToDevice);
-        if (te != hipSuccess) {
-            fail(MPPI_ERR_HIP, "fused step parameters: %s", hipGetErrorString(te));
-            mppi_destroy(e);
-            return MPPI_ERR_HIP;
-        }
-        e->fuse = true;
     }
     *out = e;
     return MPPI_OK;
@@ -1115,8 +1060,7 @@ void mppi_destroy(mppi_engine* e) {
     if (e->comm) rccl().destroy(e->comm);
     void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps,
-                   e->d_ff, e->d_cnt};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -1318,14 +1262,12 @@ mppi_status mppi_exchange(mppi_engine* e) {
 }
 
 // the rollout's per-block partial records (DevParams::hdr / rdata layout)
-namespace {
-void block_records(const mppi_engine* e, FinParams& f) {
+static void block_records(const mppi_engine* e, FinParams& f) {
     const int64_t nb = e->dp.nb, H = e->H;
     f.nrec = (int32_t)nb;
     f.hdr = e->d_hdr; f.hdr_vs = nb * 4; f.hdr_rs = 4;
     f.dat = e->d_rdata; f.d_vs = (int64_t)e->A * nb * H; f.d_as = nb * H; f.d_rs = H;
 }
-}  // namespace
 
 // The finalize's record source: the rollout blocks' records, or the exchange slots of a shard.
 static void final_records(const mppi_engine* e, FinParams& f) {
@@ -1351,9 +1293,6 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
     p.noise_in = d_noise;
     p.vc0 = e->h_vc[0];
     p.step_ctr = e->step_ctr;
-    // a shard's pack runs in the rollout's own launch when the step is fused (its last blocks)
-    const bool fused_pack = sharded(e) && e->fuse;
-    if (fused_pack) p.ff = e->d_ff + kTailPack;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
     int rc = mppi_launch_rollout(&p, e->threads, e->stream);
@@ -1364,7 +1303,7 @@ mppi_status mppi_rollout(mppi_engine* e, const float* d_noise) {
         e->roll_pairs.emplace_back(e0, e1);
         if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
     }
-    if (sharded(e) && !fused_pack) {   // fold this shard's block records into its exchange slot
+    if (sharded(e)) {   // fold this shard's block records into its exchange slot
         FinParams f = e->fp;
         pack_fields(e, f);
         f.tail = e->d_tail + kTailPack;
@@ -1409,40 +1348,6 @@ static mppi_status finalize_impl(mppi_engine* e, bool record_out) {
 mppi_status mppi_finalize(mppi_engine* e) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     return finalize_impl(e, true);
-}
-
-// One fused step through HIP (an unsharded engine with e->fuse): ONE k_rollout launch whose last
-// blocks fold the records and finalise (mppi_rollout.h fused_tail), with finalize_impl's
-// bookkeeping (sequence number, output event, step counter).
-static mppi_status fused_step(mppi_engine* e, const float* d_noise, bool record_out) {
-    if (use_device(e)) return MPPI_ERR_HIP;
-    DevParams p = e->dp;
-    p.noise_in = d_noise;
-    p.vc0 = e->h_vc[0];
-    p.step_ctr = e->step_ctr;
-    p.ff = e->d_ff + ((e->out_dbg == 1 && !record_out) ? kTailScratch : kTailFinal);
-    p.seq = 0u;   // no completion records for unread steps
-    if (record_out && !e->no_flag_dbg) {   // as finalize_impl: a fresh value per read step, never 0
-        p.seq = ++e->seq_ctr & 0x7FFFFFFFu;
-        if (p.seq == 0u) p.seq = ++e->seq_ctr & 0x7FFFFFFFu;
-    }
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
-    const int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-    if (rc != 0) return fail(MPPI_ERR_HIP, "fused step launch failed (%d: %s)", rc,
-                             rc > 0 ? hipGetErrorString((hipError_t)rc) : "no fused kernel for this model/A/H");
-    if (e->timing) {
-        HIP_TRY(hipEventRecord(e1, e->stream));
-        e->roll_pairs.emplace_back(e0, e1);
-        if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
-    }
-    if (record_out) e->out_seq = p.seq;
-    if (record_out) HIP_TRY(hipEventRecord(e->ev_out, e->stream));
-    ++e->step_ctr;
-    e->out_pending = record_out;
-    e->aql_out = false;
-    e->aql_call = false;
-    return MPPI_OK;
 }
 
 // True when every output record of the pending read step carries its sequence number (the
@@ -1652,10 +1557,6 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         HIP_TRY(hipMemcpyAsync(e->d_noise_in, h_noise, n * sizeof(float), hipMemcpyHostToDevice, e->stream));
         dn = e->d_noise_in;
     }
-    if (e->fuse && !sharded(e)) {
-        if ((st = fused_step(e, dn, true)) != MPPI_OK) return st;
-        return mppi_read_outputs(e, out, u0, stats);
-    }
     if ((st = mppi_rollout(e, dn)) != MPPI_OK) return st;
     if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
     if ((st = mppi_finalize(e)) != MPPI_OK) return st;
@@ -1679,7 +1580,6 @@ static const char* aql_ineligible(const mppi_engine* e, bool batch = false) {
 // native dispatch it is relative to the dispatch id (kNoiseStepFromId in the noise-mode word).
 constexpr uint32_t kRollStepOff = 8;
 constexpr int32_t kNoiseStepFromId = 0x100;   // = mppi_device.h
-constexpr int32_t kNoiseStepFromId1 = 0x200;  // the same for single-packet (fused) steps
 
 // n steps as native AQL packets (mppi_aql.cpp).  *used = false: the caller runs them through
 // HIP (auto mode, native dispatch unavailable for this engine; e->aql_why says why).
@@ -1718,16 +1618,14 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     p.noise_in = nullptr;
     p.vc0 = e->h_vc[0];
     p.step_ctr = 0u;                      // (set by step_prepare: relative to the dispatch id)
-    const bool fused = e->fuse;           // one packet per step (the rollout finalises itself)
-    p.noise_mode |= fused ? kNoiseStepFromId1 : kNoiseStepFromId;
-    if (fused) { p.ff = e->d_ff + kTailFinal; p.seq = 0u; }
+    p.noise_mode |= kNoiseStepFromId;
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // completion: the batch's signal, not a flag
     final_records(e, f);
     mppi_aql::set_capture(&roll);
     int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-    if (rc == 0 && !fused) {
+    if (rc == 0) {
         mppi_aql::set_capture(&fin);
         rc = mppi_launch_finalize(&f, e->stream);
     }
@@ -1735,7 +1633,7 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
     std::string err;
     const auto c2 = now();
-    const int pr = mppi_aql::step_prepare(e->aql, roll, fused ? nullptr : &fin, e->step_ctr, kRollStepOff, &err);
+    const int pr = mppi_aql::step_prepare(e->aql, roll, fin, e->step_ctr, kRollStepOff, &err);
     const auto c3 = now();
     if (pr == -2) {   // not dispatchable natively (a kernel the code objects lack, hidden arguments)
         e->aql_off = true;
@@ -1794,9 +1692,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
     p.noise_in = nullptr;
     p.vc0 = e->h_vc[0];
     p.step_ctr = 0u;
-    const bool fused = e->fuse;   // one packet per call (the rollout finalises itself)
-    p.noise_mode |= fused ? kNoiseStepFromId1 : kNoiseStepFromId;
-    if (fused) { p.ff = e->d_ff + kTailFinal; p.seq = kSeqFromVc; }
+    p.noise_mode |= kNoiseStepFromId;
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = kSeqFromVc;
@@ -1819,7 +1715,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
         e->call_cached = false;
         mppi_aql::set_capture(&roll);
         int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0 && !fused) {
+        if (rc == 0) {
             mppi_aql::set_capture(&fin);
             rc = mppi_launch_finalize(&f, e->stream);
         }
@@ -1843,7 +1739,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
                              (uint32_t)offsetof(VehicleConst, _pad);
     std::string err;
     uint32_t seq = 0;
-    const int pr = mppi_aql::step_call(e->aql, roll, fused ? nullptr : &fin, e->step_ctr, kRollStepOff, seq_off, &seq, &err);
+    const int pr = mppi_aql::step_call(e->aql, roll, fin, e->step_ctr, kRollStepOff, seq_off, &seq, &err);
     if (pr == -2) {
         e->aql_off = true;
         e->aql_why = err;
@@ -1869,10 +1765,6 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     mppi_status st = run_steps_aql(e, n, &used);
     if (st != MPPI_OK || used) return st;
     for (int i = 0; i < n; ++i) {
-        if (e->fuse && !sharded(e)) {
-            if ((st = fused_step(e, nullptr, i == n - 1)) != MPPI_OK) return st;
-            continue;
-        }
         mppi_status st = mppi_rollout(e, nullptr);
         if (st != MPPI_OK) return st;
         if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
@@ -1897,10 +1789,6 @@ mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us,
     DevParams p = e->dp;
     p.vc0 = e->h_vc[0];
     p.step_ctr = e->step_ctr;
-    // fused steps: the timed rollout is the fused launch a step runs -- its tail finalising into
-    // the device scratch outputs (unsharded; no finalize launch then) or packing the shard's slot
-    const bool fused_final = e->fuse && !sharded(e);
-    if (e->fuse) p.ff = e->d_ff + (fused_final ? kTailScratch : kTailPack);
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // the throughput path's finalize (no completion flag)
@@ -1930,13 +1818,13 @@ mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us,
     KT_TRY(hipEventRecord(ev[0], e->stream));
     for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_rollout(&p, e->threads, e->stream);
     KT_TRY(hipEventRecord(ev[1], e->stream));
-    for (int i = 0; i < n && rc == 0 && !fused_final; ++i) rc = mppi_launch_finalize(&f, e->stream);
+    for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_finalize(&f, e->stream);
     KT_TRY(hipEventRecord(ev[2], e->stream));
     // the kernels as a control step runs them: rollout after finalize (u_prev and the
-    // records just written, cold in the other XCDs' L2); a fused step is its one launch
+    // records just written, cold in the other XCDs' L2)
     for (int i = 0; i < n && rc == 0 && pair_us; ++i) {
         rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0 && !fused_final) rc = mppi_launch_finalize(&f, e->stream);
+        if (rc == 0) rc = mppi_launch_finalize(&f, e->stream);
     }
     KT_TRY(hipEventRecord(ev[3], e->stream));
     KT_TRY(hipMemcpyAsync(e->d_u_prev, saved, ub, hipMemcpyDeviceToDevice, e->stream));
@@ -2022,10 +1910,9 @@ mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us
 
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len) {
     if (!e || !buf || len <= 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_dispatch_info: bad arguments");
-    snprintf(buf, (size_t)len, "%s%s; calls: %s%s%s; step: %s%s", e->aql_why.empty() ? "aql" : "hip: ",
-             e->aql_why.c_str(), e->calls_native ? "aql (arguments in " : "hip",
-             e->calls_native ? mppi_aql::step_call_memory(e->aql) : "", e->calls_native ? ")" : "",
-             e->fuse ? (sharded(e) ? "fused rollout+pack" : "fused") : "two kernels: ", e->fuse ? "" : e->fuse_why.c_str());
+    snprintf(buf, (size_t)len, "%s%s; calls: %s%s%s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str(),
+             e->calls_native ? "aql (arguments in " : "hip", e->calls_native ? mppi_aql::step_call_memory(e->aql) : "",
+             e->calls_native ? ")" : "");
     return MPPI_OK;
 }
 
@@ -2103,6 +1990,17 @@ mppi_status mppi_get_weighted_noise(mppi_engine* e, float* raw, float* smoothed)
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
     const size_t n = sizeof(float) * e->V * e->H * e->A;
+    // w_eps and its SavGol of the records the last step combined (its block records, or the
+    // shard's all-reduced exchange slots): k_finalize in READBACK mode, which writes only these.
+    // The step's own finalize stores no readback copies (no stores that only a readback needs on
+    // the latency path, and none left dirty in an XCD's L2 across a native batch).
+    FinParams f = e->fp;
+    f.mode = 2;
+    f.seq = 0u;
+    final_records(e, f);
+    f.tail = e->d_tail + kTailReadback;
+    const int rc = mppi_launch_finalize(&f, e->stream);
+    if (rc != 0) return fail(MPPI_ERR_HIP, "weighted-noise readback launch failed (%d)", rc);
     if (raw) HIP_TRY(hipMemcpyAsync(raw, e->d_wraw, n, hipMemcpyDeviceToHost, e->stream));
     if (smoothed) HIP_TRY(hipMemcpyAsync(smoothed, e->d_wsmooth, n, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));

@@ -119,13 +119,7 @@ struct DevParams {
     float q_g;                    // gravity magnitude, g = (0, 0, -q_g)
     int32_t q_literal_jinv;       // t >= 1 applies inv(J) to the body rates, as the commented loop
                                   // (drone_mppi.py:73-76); 0 = J at every step
-    // fused step (k_rollout FUSE instantiations): the launch's last-arriving blocks fold the
-    // records and run the finalize (FINAL) or the shard's pack (PACK) in the same launch
-    const struct FusedFin* ff;    // device-resident; null = records only (a k_finalize launch follows)
-    uint32_t seq;                 // FINAL: the read step's sequence number (0: none; kSeqFromVc: native call)
-    int32_t _pad_ff;
 };
-
 constexpr int kStamps = 16;
 
 // The finalize tail's parameters, device-resident: written once at create (one copy per
@@ -149,24 +143,10 @@ struct FinTail {
     int32_t nslots, myslot, P, pad_;
     float sg[kMaxW];
 };
-enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailSlots = 3 };
-
-// What the fused step's folding blocks need (k_rollout FUSE, mppi_rollout.h fused_tail): the
-// finalize's launch description, device-resident (written at create and at exchange binding),
-// and the per-vehicle arrival counters.  fin_body runs with CW = 16 (the window of a t-slice and
-// its SavGol halo fits 16 columns: savgol_window <= 9) and NT = nt threads.
-struct FusedFin {
-    const float* hdr;                  // the block records (DevParams hdr / rdata layout)
-    const float* dat;
-    const FinTail* tail;              // FINAL into the outputs, or the shard's PACK
-    uint32_t nrec_H, geo;              // as k_finalize's arguments
-    int32_t hdr_rs, d_rs, d_as, hdr_vs, d_vs;
-    int32_t nfold;                     // folding blocks per vehicle: A * t-slices
-    int32_t nt;                        // fin_body block size: 256 or 512
-    int32_t win;                       // SavGol window (5 and 9 specialised, else the generic loop)
-    unsigned long long* cnt;           // (V) arrival counters: 64-bit, monotonic (nb per step)
-    unsigned long long* stamps;        // diagnostic (MPPI_STAMPS), else null
-};
+// FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
+// timing, probes), READBACK (mppi_get_weighted_noise: w_eps and its SavGol of the records as they
+// stand, nothing else written)
+enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTailSlots = 4 };
 // k_finalize's sequence argument: this value = take the step's sequence number from the vehicle
 // constants (VehicleConst::_pad[0]; native control calls, mppi_aql.cpp).  HIP-path sequence
 // numbers stay below 2^31, native ones have bit 31 set: the two never meet in the flags.

@@ -25,10 +25,7 @@ namespace {
 // relative to the dispatch id -- step = arg + (dispatch id >> 1) -- so one argument block,
 // written once, serves every (rollout, finalize) pair the engine's queue runs
 constexpr int32_t kNoiseStepFromId = 0x100;
-// the same for a queue of single-packet steps (the fused step: step = arg + dispatch id)
-constexpr int32_t kNoiseStepFromId1 = 0x200;
 __device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg) {
-    if (noise_arg & kNoiseStepFromId1) return step_arg + (uint32_t)mppi_dispatch_id();
     return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
 }
 
@@ -62,36 +59,25 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return (T*)(((uint64_t)hi << 32) | lo);
 }
 
-// Block-uniform values into SGPRs (v_readfirstlane; free when the value is scalar already).  In
-// a kernel that stores to global memory the compiler cannot load its parameter blocks with
-// scalar loads (fin_body inside the fused rollout), and an "s" asm operand fed by a vector load
-// is an illegal VGPR-to-SGPR copy.
-__device__ __forceinline__ int32_t rfl(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-__device__ __forceinline__ int64_t rfl(int64_t x) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-template <typename T>
-__device__ __forceinline__ T* rfl(T* p) { return uniform_ptr(p); }
-
-// A run of n consecutive floats from LDS (src) to dst[0..n), dst wave-uniform, written through:
-// thread i stores elements 4i..4i+3 as ONE 16 B sc1 buffer store where all four exist and dst + 4i
-// is 16 B aligned (a block's costs are whole 64 B lines at the common shapes: no partial-line
-// writes, which HBM merges slowly), else one 4 B sc1 store per element.
-__device__ __forceinline__ void st_dev_run(float* dst_uniform, const float* src, int n, int i) {
+// A run of n consecutive floats from LDS (src) to base[off .. off + n), base wave-uniform (off may
+// vary per lane), written through: thread i stores elements 4i..4i+3 of the run as ONE 16 B sc1
+// buffer store where all four exist and the address is 16 B aligned (a block's costs are whole
+// 64 B lines at the common shapes: no partial-line writes, which HBM merges slowly), else one 4 B
+// sc1 store per element.
+__device__ __forceinline__ void st_dev_run(float* base_uniform, uint32_t off, const float* src, int n, int i) {
     const int e = 4 * i;
     if (e >= n) return;
-    if (e + 4 <= n && ((((uintptr_t)dst_uniform) + 4u * (uint32_t)e) & 15u) == 0u) {
+    const uint32_t o = off + (uint32_t)e;
+    if (e + 4 <= n && ((((uintptr_t)base_uniform) + 4u * o) & 15u) == 0u) {
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(dst_uniform, 0, (int)0x7FFFFFFF, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc(base_uniform, 0, (int)0x7FFFFFFF, 0x00020000);
         const float4 x = *reinterpret_cast<const float4*>(src + e);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 w = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(w, rs, 4 * e, 0, kAuxDev);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(4u * o), 0, kAuxDev);
         return;
     }
-    for (int j = 0; j < 4 && e + j < n; ++j) st_dev(dst_uniform + e + j, src[e + j]);
+    for (int j = 0; j < 4 && e + j < n; ++j) st_dev(base_uniform + o + j, src[e + j]);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic

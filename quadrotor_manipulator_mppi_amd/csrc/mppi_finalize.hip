@@ -4,7 +4,7 @@
 // kernel in PACK mode folds a shard's records into its exchange slot.
 #include <algorithm>
 
-#include "mppi_finbody.h"
+#include "mppi_device.h"
 
 using namespace mppi;
 
@@ -23,6 +23,60 @@ using namespace mppi;
 // MI355X (profiles/r01/finalize_threads_s3.txt): arm C3 (256 records) 5.91 -> 5.26 us at
 // 256 threads, the V=8 fleet (128 records per vehicle) 10.58 -> 5.46 us at 128, whole-body
 // K=8192 (512 records) best at 512.
+constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 waves)
+constexpr int kMaxRec = 4096;
+// timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
+// outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor), 32 skips
+// the u_prev update, 64 skips the tail parameters' kernel-argument loads, 128 the final drain
+#ifndef MPPI_FIN_KO
+#define MPPI_FIN_KO 0
+#endif
+// XCDs the finalize's blocks run on (8; 4 = the first four, see the block map in k_finalize)
+#ifndef MPPI_FIN_XCDS
+#define MPPI_FIN_XCDS 8
+#endif
+
+#if defined(MPPI_STAMPS) && !defined(MPPI_TIMELINE)
+#define FSTAMP(i)                                                                    \
+    do {                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+        if (pk.stamps && threadIdx.x == 0)                                           \
+            pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + (i)] =               \
+                __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+    } while (0)
+#define FSTAMPRT(i) do { } while (0)
+#elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: block start / end (wave 0) in wall-clock time, the
+                             // XCD in slot 15, the first chunk's loads issued + tail pinned (slot 7)
+                             // and the wave fold's end (slot 1: records combined)
+#define FSTAMPRT(i)                                                                  \
+    do {                                                                             \
+        if (pk.stamps && threadIdx.x == 0) {                                         \
+            pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + (i)] =               \
+                __builtin_amdgcn_s_memrealtime();                                    \
+            if ((i) == 13)                                                           \
+                pk.stamps[(((size_t)v * A + a) * ts + sl) * kStamps + 15] =            \
+                    (unsigned long long)__builtin_amdgcn_s_getreg(0xF814);           \
+        }                                                                            \
+    } while (0)
+#define FSTAMP(i) do { if ((i) == 1 || (i) == 7) FSTAMPRT(i); } while (0)
+#else
+#define FSTAMP(i) do { } while (0)
+#define FSTAMPRT(i) do { } while (0)
+#endif
+
+// Block = 8 waves.  Lane (g, q) of wave wv holds window column q (CW = 16/32/64
+// columns) of the records gr, gr + TR, gr + 2 TR, ... where gr = wv*ROWS + g is
+// its global row and TR = 8*ROWS the row count.  Records are consumed in chunks
+// of TR*kNPT with every load of a chunk in flight; each lane keeps a running
+// rho_t (online softmin, like the rollout).  Rows are folded inside each wave
+// (xor shuffles, DPP), the 8 waves through LDS behind ONE barrier, and wave 0
+// finishes alone: w_eps, SavGol by lane shuffles (WIN taps, template), u_prev,
+// outputs.
+// The leading scalar arguments (through the step's sequence number) are preloaded into
+// SGPRs (build.py: 14 dwords); the tail's parameters come from the device-resident FinTail
+// (L2-hot across steps), so a FINAL launch of one vehicle reads nothing else of its
+// kernel-argument block.  pk carries the PACK-mode fields and the diagnostic stamps.
 template <int CW, int WIN, int NT>
 __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_base,
                                                           const float* __restrict__ dat_base,
@@ -32,6 +86,17 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                                                           const int32_t d_as, const int32_t hdr_vs,
                                                           const int32_t d_vs, const uint32_t seq_arg,
                                                           const FinParams pk) {
+    constexpr int NWV = NT / 64;
+    constexpr int ROWS = 64 / CW;          // rows per wave
+    constexpr int TR = NWV * ROWS;         // rows per block
+    constexpr int kNPT = 16;
+    __shared__ float wcol[NWV][CW];
+    __shared__ float wrho[NWV], wnan[NWV], weta[NWV], weta2[NWV];
+    __shared__ float wsg[96];   // wave 0: w over the window + reflected pads (SavGol taps by LDS reads)
+    const FinParams& p = pk;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = (int)(nrec_H & 0xFFFFu), H = (int)(nrec_H >> 16);
+    const int tsz = (int)(geo & 0xFFu), hf = (int)((geo >> 8) & 0xFFu), ts = (int)((geo >> 16) & 0xFFu);
     const int A = (int)(geo >> 24);
     // XCD-aware block map: the dispatcher deals blocks round robin over the 8 XCDs (block b
     // on XCD b mod 8).  Dim a lives on XCD a mod X (X = MPPI_FIN_XCDS of them), every slice of
@@ -44,9 +109,306 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     const int sl = (na == 1) ? j8 : (na == 2) ? (j8 >> 1) : j8 / na;
     const int a = x8 + MPPI_FIN_XCDS * (j8 - sl * na), v = blockIdx.y;
     if (x8 >= MPPI_FIN_XCDS || a >= A) return;
-    if (MPPI_FIN_KO & 16) { if (threadIdx.x == 0) pk.u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
-    fin_body<CW, WIN, NT>(a, sl, v, hdr_base, dat_base, tail, nrec_H, geo, hdr_rs, d_rs, d_as, hdr_vs, d_vs, seq_arg,
-                          pk.stamps);
+    if (MPPI_FIN_KO & 16) { if (tid == 0) p.u_prev[blockIdx.x] = 0.0f; return; }   // timing knockout: launch floor
+    FSTAMPRT(13);
+    FSTAMP(0);
+    const int t_lo = sl * tsz, t_hi = min(H, t_lo + tsz);
+    const int w0 = max(0, t_lo - hf), w1 = min(H, t_hi + hf), W = w1 - w0;   // window [w0, w1), W <= CW
+    // (both bases and the header range kept in SGPRs: in a build where the compiler put one
+    // in VGPRs, every record load became a waterfall loop over a "divergent" resource)
+    const float* hdr = uniform_ptr(hdr_base + (size_t)v * (uint32_t)hdr_vs);
+    const float* col = uniform_ptr(dat_base + (size_t)v * (uint32_t)d_vs + (size_t)a * d_as + w0);
+    const FinTail& T = *tail;
+    const int g = lane / CW, q = lane - g * CW, gr = wv * ROWS + g;
+    const bool qv = q < W;
+    // wave 0's u_prev over the window (lane q <-> t = w0 + q, incl. the OLD u_prev[0],
+    // mppi.py:157) and the vehicle constants of the outputs (slice 0 of each dim, lane 0) are
+    // loaded AFTER the first chunk of record loads is issued (pin_tail below): they need the
+    // tail's pointers (an s_load round trip, then their own), and issued first they held the
+    // record loads behind both -- the register allocator paired a pending u_prev/vc load with
+    // the record offsets, and the whole wave waited for vmcnt(0) before its first record load
+    float u_old = 0.0f, x0f = 0.0f, v0f = 0.0f;
+    double x0d = 0.0, v0d = 0.0;
+    float* up = nullptr;
+
+    // The tail's parameters (FinTail), read into SGPRs while the record loads fly: left to
+    // the compiler, each was an s_load waited for on the spot in wave 0's tail (15 serial
+    // scalar round trips).  The empty asm makes every value opaque, so it is neither
+    // re-loaded later nor sunk to its use.
+    float coef = 0.0f, dt = 0.0f, dt2 = 0.0f;
+    int32_t mode = 0, model = 0, qoff = 0, nq = 0, sf64 = 0, odim = 0;
+    const uint32_t seq = seq_arg;
+    // native control calls (mppi_aql.cpp): the step's sequence number travels with the vehicle
+    // constants (VehicleConst::_pad[0], written by the host into the rollout's arguments, handed
+    // over by the rollout's block 0), so the finalize's own argument block stays static
+    uint32_t seqv = seq;
+    float *wraw = nullptr, *wsmooth = nullptr, *u0p = nullptr, *stats = nullptr;
+    double* outp = nullptr;
+    uint32_t* flags = nullptr;
+    const VehicleConst* vcb = nullptr;
+    float sg[WIN > 0 ? WIN : 1];
+    auto pin_tail = [&]() {
+        // every load issues first, then two empty asms consume them (one wait): pinned one
+        // by one, each load was followed by its own s_waitcnt, ~20 serial round trips
+        coef = T.coef; dt = T.dt; dt2 = T.dt2;
+        mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
+        wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
+        up = T.u_prev; vcb = T.vc;
+        if constexpr (WIN > 0) {
+#pragma unroll
+            for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
+        }
+        asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
+                          "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
+                          "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb));
+        if constexpr (WIN == 9)
+            asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
+                              "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
+        else if constexpr (WIN == 5)
+            asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]));
+        // then the loads that need those pointers (global address space: a flat load also
+        // counts in lgkmcnt, so every later scalar wait would wait for it too)
+        up += (size_t)v * H * A;
+        // (device-scope loads: the previous finalize's u_prev, the rollout's handed-over vc)
+        if (wv == 0 && q < W && g == 0) u_old = ld_dev(up + (w0 + q) * A + a);
+        if (tid == 0 && sl == 0) {
+            const VehicleConst* vcp = vcb + v;
+            x0f = ld_dev(vcp->pos0f + a); v0f = ld_dev(vcp->vel0f + a);
+            x0d = ld_dev(vcp->pos0 + a); v0d = ld_dev(vcp->vel0 + a);
+            if (seq == kSeqFromVc) seqv = ld_dev((const uint32_t*)vcp->_pad);   // (its bits)
+        }
+    };
+    // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
+    // column of a row group, so each lane carries them and the wave fold runs over row groups
+    // only.  eta in fp32, like the reference's torch.sum of the fp32 exponentials
+    // (mppi.py:184-188): <= 16 terms per lane, then 2 + 3 (8 waves) folds.
+    float rho_t = INFINITY, acc = 0.0f, nanflag = 0.0f, eta = 0.0f, eta2 = 0.0f;
+    // Record loads through buffer resources over this vehicle's headers and this (dim,
+    // window)'s body columns: each load is one 32-bit VGPR offset (a full-rate add per row)
+    // instead of a 64-bit address (v_mad_u64_u32 + v_lshl_add_u64, both quarter-rate: ~380
+    // cycles of address math ahead of the first load).  Rows past n are masked at use (okm);
+    // their offsets run past the resources' ranges, which read 0 instead of faulting.
+    const uint32_t hrs_b = (uint32_t)hdr_rs * 4u, drs_b = (uint32_t)d_rs * 4u;
+    const __amdgpu_buffer_rsrc_t hrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hdr), 0, __builtin_amdgcn_readfirstlane((int)((uint32_t)n * hrs_b)),
+                                          0x00020000);
+    // (the range is block-uniform, but its W reaches the compiler through VGPR math: without
+    // readfirstlane every body load became a waterfall loop over a "divergent" resource)
+    const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(col), 0, __builtin_amdgcn_readfirstlane((int)((uint32_t)(n - 1) * drs_b + (uint32_t)W * 4u)),
+        0x00020000);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (int base = 0; base < n; base += TR * kNPT) {
+        float4 hd[kNPT];
+        float xv[kNPT];
+        uint32_t okm = 0;   // rows past n are masked at use: a select on the loaded value
+                            // here made the compiler wait for each load in turn
+        const uint32_t r0 = (uint32_t)(base + gr);
+        const uint32_t hoff = r0 * hrs_b, coff = r0 * drs_b + (uint32_t)(qv ? q : 0) * 4u;
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) {
+            okm |= (uint32_t)(r0 + (uint32_t)(i * TR) < (uint32_t)n) << i;
+            const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(hrsrc, (int)(hoff + (uint32_t)(i * TR) * hrs_b), 0, kAuxDev);
+            hd[i] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
+            xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crsrc, (int)(coff + (uint32_t)(i * TR) * drs_b), 0, kAuxDev));
+        }
+        if (base == 0 && !(MPPI_FIN_KO & 64)) {   // (64: timing knockout, tail parameters not loaded)
+            __builtin_amdgcn_sched_barrier(0);   // the first chunk's record loads issue first
+            pin_tail();
+        }
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i)
+            if (!((okm >> i) & 1u)) hd[i].x = INFINITY;   // f = 0: y, z and xv drop out
+        FSTAMP(7);
+        float m = INFINITY;
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) { m = fminf(m, hd[i].x); nanflag = fmaxf(nanflag, hd[i].w); }
+        // the body terms are accumulated outside the branch: used only inside it, the
+        // compiler sank the body loads into it, behind a wait for every header load (two
+        // memory round trips instead of one).  f = 0 adds exactly nothing (bodies are finite:
+        // sums of weighted noise, 0 for a block without a finite cost).
+        float fr[kNPT];
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) fr[i] = 0.0f;
+        if (m < INFINITY) {
+            const float rn = fminf(rho_t, m);
+            if (rho_t < INFINITY) {   // rescale the running sums to the new reference
+                const float sc = __expf(coef * (rho_t - rn));
+                acc *= sc;
+                eta *= sc;
+                eta2 *= sc * sc;
+            }
+            rho_t = rn;
+#pragma unroll
+            for (int i = 0; i < kNPT; ++i) {
+                const float f = (hd[i].x < INFINITY) ? __expf(coef * (hd[i].x - rn)) : 0.0f;
+                fr[i] = f;
+                eta = fmaf(f, hd[i].y, eta);
+                eta2 = fmaf(f * f, hd[i].z, eta2);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kNPT; ++i) acc = fmaf(fr[i], xv[i], acc);
+        FSTAMP(8);
+    }
+    {   // fold the wave's row groups: rescale every lane to the wave's rho, sum the rows
+        const float rw = fold_rows<CW>(rho_t, OpMin());
+        const float sc = (rho_t < INFINITY) ? __expf(coef * (rho_t - rw)) : 0.0f;
+        acc = fold_rows<CW>(acc * sc, OpAdd());
+        const float e1 = fold_rows<CW>(eta * sc, OpAdd()), e2 = fold_rows<CW>(eta2 * (sc * sc), OpAdd());
+        const float nf = fold_rows<CW>(nanflag, OpMax());
+        if (lane < CW) wcol[wv][lane] = acc;
+        if (lane == 0) { wrho[wv] = rw; wnan[wv] = nf; weta[wv] = e1; weta2[wv] = e2; }
+    }
+    FSTAMP(1);
+    if (MPPI_FIN_KO & 8) { if (lane < CW) p.u_prev[lane] += acc + (float)eta; return; }   // timing knockout
+    lds_barrier();
+    if (wv != 0) return;
+    FSTAMP(2);
+    // wave 0: combine the 4 waves (lane q = column q)
+    float rho = wrho[0], nanf = wnan[0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) { rho = fminf(rho, wrho[w]); nanf = fmaxf(nanf, wnan[w]); }
+    float N = 0.0f;
+    eta = 0.0f; eta2 = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+        const float f = (wrho[w] < INFINITY) ? __expf(coef * (wrho[w] - rho)) : 0.0f;
+        N = fmaf(f, (lane < CW) ? wcol[w][lane] : 0.0f, N);
+        eta = fmaf(f, weta[w], eta);
+        eta2 = fmaf(f * f, weta2[w], eta2);
+    }
+    FSTAMP(3);
+    const int t = w0 + lane;              // this lane's time index (lanes < W)
+    const bool own = lane < W && t >= t_lo && t < t_hi;
+    if (mode == 1) {   // PACK raw sums into this shard's exchange slot
+        // the slot fields in one scalar round trip (each was its own wait in the tail)
+        float* dst = T.dst;
+        float* xbase = T.xbase;
+        int64_t xslot = T.xslot;
+        int32_t nslots = T.nslots, myslot = T.myslot, P = T.P;
+        asm volatile("" : "+s"(dst), "+s"(xbase), "+s"(xslot), "+s"(nslots), "+s"(myslot), "+s"(P));
+        dst += (size_t)v * P;
+        if (a == 0 && sl == 0 && lane == 0) {
+            dst[0] = rho; dst[1] = eta; dst[2] = eta2; dst[3] = nanf;
+        }
+        if (own) dst[kHdr + a * H + t] = N;
+        for (int s = 0; s < nslots; ++s) {   // zero the other shards' slots (x + 0 is exact)
+            if (s == myslot) continue;
+            float* z = xbase + (size_t)s * xslot + (size_t)v * P;
+            if (a == 0 && sl == 0 && lane < kHdr) z[lane] = 0.0f;
+            if (own) z[kHdr + a * H + t] = 0.0f;
+        }
+        FSTAMPRT(14);
+        return;
+    }
+
+    // FINAL: w_eps = N/eta over the window, SavGol, u += w_eps
+    const float etaf = (nanf > 0.0f) ? NAN : eta;
+    const float w = __fdividef(N, etaf);
+    FSTAMP(4);
+    // SavGol with the reference's symmetric pad (svg_filter.py:58: index -i-1 left of 0,
+    // 2H-1-i right of H-1; one reflection suffices, create checks H > window/2): w goes to
+    // LDS at kPad + (t - w0), and the lanes within hf of an edge of the horizon also write
+    // their mirror position, so every owned lane reads its WIN taps at consecutive addresses
+    // (immediate offsets, one wait) -- no per-tap index arithmetic, no ds_bpermute.
+    constexpr int kPad = kMaxW / 2;   // >= hf for every window create accepts (<= MPPI_MAX_SAVGOL)
+    static_assert(kPad + 64 + kMaxW / 2 <= (int)(sizeof(wsg) / sizeof(float)),
+                  "wsg holds the widest window: kPad + W (<= 64) + hf");
+    float sm = 0.0f;
+    if (lane < W) {
+        wsg[kPad + lane] = w;
+        if (w0 == 0 && t < hf) wsg[kPad - 1 - t] = w;                      // left pad
+        if (w1 == H && t >= H - hf) wsg[kPad + 2 * H - 1 - t - w0] = w;    // right pad
+    }
+    wave_lds_handoff();
+    {
+        const float* src = wsg + kPad + lane - hf;
+        if constexpr (WIN > 0) {
+#pragma unroll
+            for (int j = 0; j < WIN; ++j) sm = fmaf(sg[j], src[j], sm);
+        } else {
+            for (int j = 0; j < T.window; ++j) sm = fmaf(T.sg[j], src[j], sm);
+        }
+    }
+    FSTAMP(5);
+    if (mode == 2) {   // READBACK (mppi_get_weighted_noise): w_eps and its SavGol, nothing else
+        if (own) {
+            wraw[((size_t)v * H + t) * A + a] = w;
+            wsmooth[((size_t)v * H + t) * A + a] = sm;
+        }
+        return;
+    }
+    const float un = u_old + sm;
+    if (own) {
+        // written through at device scope (the next rollout reads it on every XCD), drained at
+        // the end: the native dispatch's finalize packets then need no release (mppi_aql.cpp)
+        if (!(MPPI_FIN_KO & 32))   // (32: timing knockout, u_prev not written)
+            __hip_atomic_store(up + t * A + a, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!(MPPI_FIN_KO & 2) && sl == 0 && lane == 0) {   // t = 0 lives in lane 0 of slice 0: outputs into mapped host memory
+#pragma clang fp contract(off)
+        const float u0 = un;
+        const float uold0 = u_old;
+        u0p[(size_t)v * A + a] = u0;
+        double* out = outp + (size_t)v * odim;
+        const bool drone_dim = (model == MPPI_MODEL_DRONE) || (model == MPPI_MODEL_WHOLEBODY && a < 3);
+        double o1 = 0.0, o2 = 0.0;   // this dim's two outputs (position, velocity)
+        if (model == MPPI_MODEL_QUADROTOR) {
+            // coupled dims (thrust rotated by R(rpy)): the host forms the outputs from u0
+            // (mppi_capi.cpp quad_outputs)
+        } else if (drone_dim) {   // drone_mppi.py:168-169
+            const float x0 = x0f, v0 = v0f;
+            const float xo = (x0 + v0 * dt) + (0.5f * u0) * dt2;
+            const float vo = v0 + dt * u0;
+            o1 = xo;
+            o2 = vo;
+            out[a] = o1;
+            out[3 + a] = o2;
+        } else {           // mppi.py:157-158 (qdes uses the OLD u_prev[0])
+            const int j = a - qoff;
+            const int base = (model == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
+            const float t1 = uold0 * dt;
+            const float t2 = ((0.5f * u0) * dt) * dt;
+            const float t3 = u0 * dt;
+            if (sf64 && model == MPPI_MODEL_ARM) {
+                o1 = (x0d + (double)t1) + (double)t2;
+                o2 = v0d + (double)t3;
+            } else {
+                o1 = (double)((x0f + t1) + t2);
+                o2 = (double)(v0f + t3);
+            }
+            out[base + j] = o1;
+            out[base + nq + j] = o2;
+        }
+        const float ess = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
+        if (a == 0) {
+            float* st = stats + (size_t)v * 4;
+            st[0] = rho;
+            st[1] = eta;
+            st[2] = ess;
+            st[3] = nanf;
+        }
+        // Completion of a read step (seq != 0; mppi_run_steps' earlier steps have none): tagged
+        // output records in mapped host memory, each ONE 16 B store carrying the step's sequence
+        // number beside its values -- (o1, u0, seq) and (o2, nan flag, seq) per dim, (rho, eta,
+        // ess, seq) per vehicle -- so the host takes the values from a record whose own tag it
+        // checks (mppi_capi.cpp wait_outputs / mppi_read_outputs) and nothing needs ordering
+        // against anything else: no system-scope fence (an L2 writeback of ~1.5 us of kernel
+        // time on the call's latency path) and no separate flag store.  The plain arrays above
+        // stay for the native batches (completed by their packet's system-scope release).
+        if (seqv != 0u) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4* rec = reinterpret_cast<u32x4*>(flags) + (size_t)v * (2 * A + 1);
+            const uint64_t b1 = (uint64_t)__double_as_longlong(o1), b2 = (uint64_t)__double_as_longlong(o2);
+            rec[2 * a] = u32x4{(uint32_t)b1, (uint32_t)(b1 >> 32), __float_as_uint(u0), seqv};
+            rec[2 * a + 1] = u32x4{(uint32_t)b2, (uint32_t)(b2 >> 32), __float_as_uint(nanf), seqv};
+            if (a == 0) rec[2 * A] = u32x4{__float_as_uint(rho), __float_as_uint(eta), __float_as_uint(ess), seqv};
+        }
+    }
+    FSTAMP(6);
+    FSTAMPRT(14);
+    if (!(MPPI_FIN_KO & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Native dispatch's check of its one assumption (mppi_aql.cpp step_create): the dispatch id the

@@ -18,7 +18,7 @@
 // Trajectories are stored as SoA planes (V,C,K,H): every store instruction of a
 // wave writes 64 consecutive floats (256 B).
 #pragma once
-#include "mppi_finbody.h"
+#include "mppi_device.h"
 
 // Timing knockouts for tools/ experiments only (MPPI_HIPCC_EXTRA=-DMPPI_KO=n; results are
 // wrong in such a build): 1 drops the integrator scans, 2 the Philox draw, 4 the FK chain,
@@ -51,6 +51,10 @@
 // wave priority by remaining rollout groups (k_rollout, iters > 1)
 #ifndef MPPI_PRIO
 #define MPPI_PRIO 1
+#endif
+// experiment knob: the costs S as plain per-lane stores (round 3), not staged write-through runs
+#ifndef MPPI_S_PLAIN
+#define MPPI_S_PLAIN 0
 #endif
 // park eps in LDS across the FK and cost (k_rollout, NA >= 7)
 #ifndef MPPI_EPS_STASH
@@ -385,64 +389,6 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 }  // namespace
 
 // =============================================================================
-// Fused step (k_rollout FUSE): the records are folded and the step finalised in the rollout's
-// own launch, by its last-arriving blocks ("fused step").  Every block, once its
-// record stores have drained (drain_stores, then a block barrier), takes a ticket on its
-// vehicle's arrival counter: one returning agent-scope add.  The counter advances by P (the
-// block count rounded up to a power of two) per step: a step's tickets are epoch + 0..nb-1, and
-// the step's last ticket also adds the P - nb padding, so pos = ticket & (P-1) needs no division.
-// The last nfold tickets of a step make their blocks the folding blocks, role j = (dim j % A,
-// t-slice j / A); a folding block whose ticket was not the step's last polls the counter (sc1
-// loads, s_sleep) until all nb blocks have arrived.  It then runs fin_body -- k_finalize's block,
-// record loads sc1 -- for its role.  This is MI355X_MICROARCH.md's valid hand-off form: sc1
-// stores drained by every storing wave, one lane's agent-scope add behind a workgroup barrier,
-// an sc1 poll by that lane, the block's other waves behind a barrier, sc1 loads.  No deadlock
-// while the nfold polling blocks and the rest of the grid fit on the chip together (create
-// keeps nfold <= 256, and every CU holds at least one rollout block).  A poll gives up after
-// 200 ms (the step's outputs then never arrive and the host reports it).
-__device__ __forceinline__ int fused_role(const FusedFin* ff, const int nb, const int v) {
-    __shared__ int s_role;
-    __syncthreads();   // every wave has drained its stores (drain_stores)
-    if (threadIdx.x == 0) {
-        unsigned long long* c = ff->cnt + v;
-        const unsigned long long P = (unsigned long long)(1u << (32 - __builtin_clz((unsigned)nb - 1u | 1u)));
-        const int F = ff->nfold;
-        const unsigned long long t = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long pos = t & (P - 1ull), end = (t - pos) + (unsigned long long)nb;
-        int role = (pos + (unsigned long long)F >= (unsigned long long)nb) ? (int)(pos + F - nb) : -1;
-        if (pos + 1ull == (unsigned long long)nb) {   // the step's last ticket: pad the epoch to P
-            if (P > (unsigned long long)nb)
-                __hip_atomic_fetch_add(c, P - (unsigned long long)nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (role >= 0) {   // wait for the step's other blocks
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < end) {
-                __builtin_amdgcn_s_sleep(2);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) { role = -1; break; }
-            }
-        }
-        s_role = role;
-    }
-    __syncthreads();
-    return __builtin_amdgcn_readfirstlane(s_role);   // (block-uniform: keep it and a, sl in SGPRs)
-}
-
-template <int WIN, int NT>
-__device__ __forceinline__ void fused_fin(const FusedFin* ff, const int a, const int sl, const int v, const uint32_t seq) {
-    fin_body<16, WIN, NT, 8>(a, sl, v, ff->hdr, ff->dat, ff->tail, ff->nrec_H, ff->geo, ff->hdr_rs, ff->d_rs, ff->d_as,
-                          ff->hdr_vs, ff->d_vs, seq, ff->stamps);
-}
-
-// the fused step's tail (after the block's record has drained)
-__device__ __forceinline__ void fused_tail(const DevParams& p, const int v) {
-    const FusedFin* ff = uniform_ptr(p.ff);
-    const int role = fused_role(ff, p.nb, v);
-    if (role < 0) return;
-    const int A = p.A, a = role % A, sl = role / A;
-    // 8 waves, 8 rows per lane in flight: 256 records per chunk of loads
-    if (ff->win == 9) fused_fin<9, 512>(ff, a, sl, v, p.seq); else fused_fin<5, 512>(ff, a, sl, v, p.seq);
-}
-
-// =============================================================================
 // k_rollout
 // =============================================================================
 // Diagnostic phase stamps (build with -DMPPI_STAMPS; see tools/stamps.md):
@@ -701,8 +647,8 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
 // arm kernel would spill at 64 and keeps the 4-wave budget -- C3 runs 2 waves per SIMD).  At the C4 shard
 // (whole-body K=8192 H=64) that is 1024 blocks x 8 waves, all resident at once: twice the
 // latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG, bool FUSE>
-__global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
+__global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_arg, const uint32_t k_off,
                                                  const int32_t noise_arg, const int32_t H_arg,
                                                  const int32_t geo_arg,
@@ -769,7 +715,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
     // the first group's standard normals overlap the loads above
     float z0[NCH][NA];
     if (noise_mode != MPPI_NOISE_INJECTED) {
-        const uint32_t kg = k_off + (uint32_t)((blockIdx.x * iters * nw + wid) * R + sub);   // group 0's k
+        const uint32_t kg = k_off + (uint32_t)((blockIdx.x * nw + wid) * R + sub);
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
             draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, step_ctr, seed_lo, seed_hi);
@@ -807,8 +753,8 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
     const int H = H_arg, K = pk.K;
     constexpr int kWs = wave_slot_floats<NA, NCH, LSEG>();
     float* const xw = smem + ((HA + 3) & ~3) + wid * kWs;   // this wave's LDS slot
-    // the block's costs, all groups (iters * nw * R consecutive k), staged for one write-through
-    // store run after the combine barrier (st_dev_run)
+    // the block's costs, nw * R consecutive k per group, staged in LDS for write-through store runs
+    // after the combine barrier (st_dev_run)
     float* const s_stage = smem + ((HA + 3) & ~3) + 8 * kWs;
     STAMP(1);
 
@@ -833,8 +779,10 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
     auto group = [&](const int it) __attribute__((always_inline)) {   // (the NCH = 4 extended kernel called it out of line: a 1.7 KB stack frame)
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
-        // a block's groups are consecutive: its costs form one run of iters * nw * R samples
-        const int g = blockIdx.x * iters + it;
+        // group it of block b: groups b, b + nb, ...  All blocks' groups of one iteration are
+        // consecutive, so the grid's concurrent trajectory stores stay in one region of the planes
+        // (consecutive groups per block scattered them: whole-body K=65536 85.5 -> 106-110 us)
+        const int g = blockIdx.x + it * p.nb;
         const int k = (g * nw + wid) * R + sub;
         const bool kval = k < K;
         const int kc = kval ? k : K - 1;   // clamped: every load stays in bounds
@@ -1164,7 +1112,8 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
         float S_mine = S_seg[0];
 #pragma unroll
         for (int s = 1; s < R; ++s) S_mine = (sub == s) ? S_seg[s] : S_mine;
-        if (kval && t0 == 0) s_stage[(it * nw + wid) * R + sub] = S_mine;
+        if (MPPI_S_PLAIN) { if (kval && t0 == 0) p.S[(size_t)v * K + k] = S_mine; }   // (experiment: round 3's plain store)
+        else if (kval && t0 == 0) s_stage[(it * nw + wid) * R + sub] = S_mine;
 
         // ---- online softmin (mppi.py:184-188) over this wave's rollouts (scalar bookkeeping)
         float m = INFINITY;
@@ -1243,11 +1192,18 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
     STAMPW(11);
     lds_barrier();
     STAMP(6);
-    {   // the block's costs: one write-through run (st_dev_run), 64 B per block at C3
-        const int nS = iters * nw * R, k0 = blockIdx.x * nS;
-        const int n = min(nS, K - k0);
-        float* const Sv = uniform_ptr(p.S + (size_t)v * K + k0);
-        for (int i = tid; 4 * i < n; i += nthr) st_dev_run(Sv, s_stage, n, i);
+    if (!MPPI_S_PLAIN && wid == nw - 1) {
+        // The block's costs: one write-through run per group (st_dev_run), nw * R consecutive
+        // samples each -- one whole 64 B line per group at R = 2 (H <= 32: C2, C3).  Issued by
+        // the block's last wave, which has the fewest record stores behind it: from wave 0 the
+        // write-through made the drone C2 step 0.2-0.3 us slower, from the last wave it is
+        // within the A/B noise of round 3's plain stores (profiles/r04/ab_cost_store_variants.txt)
+        const int nS = nw * R, q = (nS + 3) >> 2;
+        float* const Sv = uniform_ptr(p.S + (size_t)v * K);
+        for (int i = lane; i < iters * q; i += 64) {
+            const int it = i / q, k0 = (blockIdx.x + it * p.nb) * nS;
+            st_dev_run(Sv, (uint32_t)k0, s_stage + it * nS, min(nS, K - k0), i - it * q);
+        }
     }
     // rho_b = the min of the 8 wave slots, which every thread reads for f_w anyway (an LDS
     // atomicMin before the barrier cost a waterfall loop and a ds_min per wave)
@@ -1303,20 +1259,19 @@ __global__ void __launch_bounds__(512, (ONEG && !F64 && !FUSE) ? 8 : (NCH >= 4 ?
     STAMP(7);
     STAMPRT(14);
     drain_stores();
-    if constexpr (FUSE) fused_tail(p, v);
 }
 
 // =============================================================================
 // launchers
 // =============================================================================
 // the instantiation's symbol (native dispatch looks it up in the code object)
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG, bool FUSE>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
 inline void rollout_symbol(char* buf, size_t n) {
-    snprintf(buf, n, "_Z9k_rolloutILi%dELi%dELi%dELi%dELb%dELb%dELb%dELb%dELb%dEEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE",
-             MODEL, NA, NCH, LSEG, (int)F64, (int)VONE, (int)XC, (int)ONEG, (int)FUSE);
+    snprintf(buf, n, "_Z9k_rolloutILi%dELi%dELi%dELi%dELb%dELb%dELb%dELb%dEEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE",
+             MODEL, NA, NCH, LSEG, (int)F64, (int)VONE, (int)XC, (int)ONEG);
 }
 
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG, bool FUSE>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
 inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const int iters = ONEG ? 1 : p.iters;
     // (LDS: warm start, 8 wave slots, the block's cost run of iters * 8 * R floats)
@@ -1325,30 +1280,22 @@ inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>() + s_run) * sizeof(float);
     const int32_t geo = threads | (iters << 16);
     if (p.V == 1)
-        return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG, FUSE>,
-                  rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG, FUSE>, dim3(p.nb, p.V), dim3(threads), lds,
-                  s, p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev,
+        return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>,
+                  rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
+                  p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev,
                   p.joints, p);
-    return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG, FUSE>,
-              rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG, FUSE>, dim3(p.nb, p.V), dim3(threads), lds, s,
+    return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>,
+              rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
               p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev, p.joints,
               p);
 }
 
-// the single-group (ONEG) variant exists for the common kernel at NCH == 1; so does the fused
-// step (FUSE: p.ff set, the host's mppi_fusable checked the rest), in both group variants
+// the single-group (ONEG) variant exists for the common kernel at NCH == 1
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
 inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
-    if constexpr (!XC && NCH == 1) {
-        if (p.ff) {
-            if (threads != 512) return -3;
-            if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true, true>(p, threads, s);
-            return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false, true>(p, threads, s);
-        }
-        if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true, false>(p, threads, s);
-    }
-    if (p.ff) return -3;   // no fused instantiation for this kernel
-    return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false, false>(p, threads, s);
+    if constexpr (!XC && NCH == 1)
+        if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true>(p, threads, s);
+    return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false>(p, threads, s);
 }
 
 // The extended (XC) instantiation carries the extra CostManager terms, a full

@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     wave_lds_handoff();
     {   // this wave's 16 costs as one write-through 64 B run (mppi_device.h st_dev_run)
         const int k0 = kb + wid * kQR, n = min(kQR, K - k0);
-        if (lane < 4) st_dev_run(uniform_ptr(p.S + (size_t)v * K + k0), s_lds + wid * kQR, n, lane);
+        if (lane < 4) st_dev_run(uniform_ptr(p.S + (size_t)v * K), (uint32_t)k0, s_lds + wid * kQR, n, lane);
     }
     // ---- record N[a][t] = sum_k e_k eps_k[t][a], lane = t (each wave its own 16 rollouts)
     float n[kQA] = {0.0f, 0.0f, 0.0f, 0.0f};

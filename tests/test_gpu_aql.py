@@ -199,7 +199,7 @@ def test_native_control_calls_match_hip(monkeypatch, model, kw):
             np.testing.assert_array_equal(oa2, oa)
             np.testing.assert_array_equal(ua2, ua)
     assert "calls: aql" in a.dispatch_info(), a.dispatch_info()
-    assert "calls: hip;" in h.dispatch_info(), h.dispatch_info()
+    assert h.dispatch_info().endswith("calls: hip"), h.dispatch_info()
     h.close()
     a.close()
 
@@ -239,19 +239,21 @@ def test_native_dispatch_refused_when_ids_are_not_packet_indices(monkeypatch):
     monkeypatch.delenv("MPPI_DISPATCH", raising=False)
     from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
     ref = Engine(make_config("arm", device=0, seed=11, n_samples=1024, n_horizon=32))
-    monkeypatch.setenv("MPPI_AQL_PROBE_SKEW", "6")
     e = Engine(make_config("arm", device=0, seed=11, n_samples=1024, n_horizon=32))
-    for x in (ref, e):
+    for x in (ref, e):   # (the queue -- and its probe -- comes with an engine's first native batch)
         x.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
         x.set_state(_state("arm"))
+        if x is e:
+            monkeypatch.setenv("MPPI_AQL_PROBE_SKEW", "6")
         x.run_steps(4)
         x.synchronize()
+    monkeypatch.delenv("MPPI_AQL_PROBE_SKEW")
     assert "intercepted" in e.dispatch_info(), e.dispatch_info()
     assert ref.dispatch_info().startswith("aql;"), ref.dispatch_info()
     np.testing.assert_array_equal(e.get_u_prev(), ref.get_u_prev())
     oe, ue, _ = e.step(_state("arm", shift=0.01))
     orf, ur, _ = ref.step(_state("arm", shift=0.01))
     np.testing.assert_array_equal(oe, orf)
-    assert "calls: hip;" in e.dispatch_info(), e.dispatch_info()
+    assert e.dispatch_info().endswith("calls: hip"), e.dispatch_info()
     e.close()
     ref.close()
