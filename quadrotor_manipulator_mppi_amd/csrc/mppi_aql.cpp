@@ -424,7 +424,7 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 // writeback cost up to ~0.8 us per C3 step, and only a submission's FIRST packet acquires
 // (agent scope: what the host and the HIP stream wrote since the last batch -- argument
 // blocks, state, target), which saves ~0.28 us per C3 step over an acquire on every packet
-// (tools/aql_fence_probe.py).  Nothing a batch writes to device memory stays dirty in an L2
+// (tools/probes.py fences).  Nothing a batch writes to device memory stays dirty in an L2
 // either: the values read only after a batch (the costs S, the readback copies of w_eps, the
 // stored noise) are written through at device scope as well (mppi_device.h st_dev / st_dev_run).
 // Plain stores would leave them dirty across the release-free packets, and since which XCD runs

@@ -1,0 +1,332 @@
+"""GPU diagnostics for the control step (tools/, not shipped; none of it is on the product path).
+
+    python tools/probes.py <probe> [args]
+
+probes:
+  timeline <workload> [trials]   wall-clock timeline of one step (kernel spans and the gaps between
+                                 them); needs a timeline build: MPPI_HIP_LIB=<lib built with
+                                 MPPI_HIPCC_EXTRA="-DMPPI_STAMPS -DMPPI_TIMELINE"> MPPI_STAMPS=1
+                                 MPPI_EVENT_WAIT=1 MPPI_DEBUG_NO_FLAG=1
+  batch                          short-batch cost, native vs HIP dispatch: run_steps(n)+synchronize
+                                 for n = 1..200 -> per-batch intercept and per-step slope
+  fences                         C3 step rate and bit-exactness vs HIP under MPPI_AQL_FENCES
+  calls [modes]                  control-call latency p50/p90/p99, native vs HIP (comma list)
+  sequence                       (rollout, X) pair costs; MPPI_PROBE builds only
+  stamps <model> <K> <H> [threads] [nb]
+                                 per-wave phase timelines of the last rollout (stamps build,
+                                 MPPI_STAMPS=1): shader clock, wave lifetimes, per-XCD / per-CU ends
+  latency [model] [K] [H]        control-call latency split: enqueue vs read_outputs, flag vs event wait
+"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+HOME = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]
+STATES = {"arm": [0, 0, 1, 0, 0, 0, 1] + HOME + [0.0] * 7,
+          "drone": [0, 0, 1, 0, 0, 0],
+          "wholebody": [0, 0, 1, 0, 0, 0, 1] + HOME + [0.0] * 10}
+ARM_T = ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])
+
+
+def _engine(model="arm", K=4096, H=32, dispatch=None, **kw):
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    if dispatch is not None:
+        os.environ["MPPI_DISPATCH"] = dispatch
+    e = Engine(make_config(model, device=0, n_samples=K, n_horizon=H, state_f64=(model == "arm"), **kw))
+    e.set_target(*ARM_T)
+    e.set_state(np.array(STATES[model], np.float64))
+    return e
+
+
+def probe_timeline(name, trials="30"):
+    """Every rollout wave and finalize block of a timeline build stores s_memrealtime (100 MHz) at
+    its start and end; per trial the engine runs back-to-back steps and the stamps of the LAST step
+    are read: rollout first wave start .. last wave end, [PACK ..,] FINAL .., relative to the
+    rollout's first wave start.  Medians over the trials: kernel spans and launch gaps."""
+    import bench
+    from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
+    trials = int(trials)
+    w = dict(bench.WORKLOADS[name])
+    w.pop("desc")
+    w.pop("strong", None)
+    native = w.pop("native", None)
+    se = ShardedEngine(seed=1234, native=native, **w)
+    eng = se.engine
+    V = w.get("n_vehicles", 1)
+    bench.set_targets(eng, w["model"], V)
+    eng.set_state(bench.make_state(w["model"], V))
+    L = eng._L
+    L.mppi_debug_stamps.restype = C.c_int64
+    L.mppi_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    L.mppi_debug_fstamps.restype = C.c_int64
+    L.mppi_debug_fstamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+    rb = np.zeros((1 << 18, 16), np.uint64)
+    fb = np.zeros((4096, 16), np.uint64)
+    se.run_steps(50)
+    eng.synchronize()
+    periods = []   # the step period of this build (the stamps' own cost included)
+    for _ in range(5):
+        t0 = time.perf_counter()
+        se.run_steps(500)
+        eng.synchronize()
+        periods.append((time.perf_counter() - t0) / 500 * 1e9)
+    rows = []
+    for _ in range(trials):
+        se.run_steps(10)
+        eng.synchronize()
+        n = L.mppi_debug_stamps(eng._h, rb.ctypes.data, rb.shape[0])
+        r = rb[:n].astype(np.int64)
+        t0 = r[:, 13].min()
+        xcc = (r[:, 15] >> 32) & 0xF
+        row = {"roll_last_start": (r[:, 13].max() - t0) * 10.0, "roll_first_end": (r[:, 14].min() - t0) * 10.0,
+               "roll_end": (r[:, 14].max() - t0) * 10.0,
+               "roll_life_med": float(np.median(r[:, 14] - r[:, 13])) * 10.0,
+               # phases per wave: prologue (loads, LDS staging, barrier), the rollout groups, the
+               # block combine + record (slots 1 and 5 of the timeline build)
+               "roll_prologue_med": float(np.median(r[:, 1] - r[:, 13])) * 10.0,
+               "roll_philox_med": float(np.median(r[:, 10] - r[:, 13])) * 10.0,
+               "roll_staging_med": float(np.median(r[:, 1] - r[:, 10])) * 10.0,
+               "roll_groups_med": float(np.median(r[:, 5] - r[:, 1])) * 10.0,
+               "roll_combine_med": float(np.median(r[:, 14] - r[:, 5])) * 10.0}
+        for c in range(8):
+            m = xcc == c
+            if m.any():
+                row[f"roll_xcd{c}_start"] = (r[m, 13].min() - t0) * 10.0
+                row[f"roll_xcd{c}_end"] = (r[m, 14].max() - t0) * 10.0
+        for which, key in ((1, "pack"), (0, "final")):
+            m = L.mppi_debug_fstamps(eng._h, fb.ctypes.data, fb.shape[0], which)
+            f = fb[:m].astype(np.int64)
+            f = f[(f[:, 13] > 0) & (f[:, 14] >= f[:, 13])]
+            if len(f) and (f[:, 13].min() >= t0 or key == "final"):
+                row[key + "_start"] = (f[:, 13].min() - t0) * 10.0
+                row[key + "_end"] = (f[:, 14].max() - t0) * 10.0
+                row[key + "_life_med"] = float(np.median(f[:, 14] - f[:, 13])) * 10.0
+                row[key + "_last_start"] = (f[:, 13].max() - t0) * 10.0
+                row[key + "_records_med"] = float(np.median(f[:, 1] - f[:, 13])) * 10.0
+                row[key + "_issue_med"] = float(np.median(f[:, 7] - f[:, 13])) * 10.0
+                row[key + "_tail_med"] = float(np.median(f[:, 14] - f[:, 1])) * 10.0
+                fx = f[:, 15] & 0xF
+                for c in range(8):
+                    m = fx == c
+                    if m.any():
+                        row[f"{key}_xcd{c}_start"] = (f[m, 13].min() - t0) * 10.0
+        rows.append(row)
+    med = {k: float(np.median([r[k] for r in rows if k in r])) for k in rows[0].keys()}
+    out = {"workload": name, "trials": trials, "dispatch": eng.dispatch_info(),
+           "ns_median": {k: round(v) for k, v in med.items()}}
+    if "final_start" in med:
+        gaps = {"rollout_span": med["roll_end"]}
+        prev = med["roll_end"]
+        if "pack_start" in med:
+            gaps["gap_rollout_pack"] = med["pack_start"] - prev
+            gaps["pack_span"] = med["pack_end"] - med["pack_start"]
+            prev = med["pack_end"]
+        gaps["gap_to_final"] = med["final_start"] - prev
+        gaps["final_span"] = med["final_end"] - med["final_start"]
+        gaps["step_to_final_end"] = med["final_end"]
+        gaps["step_period"] = float(np.median(periods))
+        gaps["gap_final_to_next_rollout"] = gaps["step_period"] - med["final_end"]
+        out["us"] = {k: round(v / 1e3, 3) for k, v in gaps.items()}
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
+def probe_batch():
+    """Median wall time of run_steps(n); synchronize() after an untimed priming batch each time:
+    the intercept is the per-batch bracket (first kernel start + completion wake-up), the slope
+    the per-step time."""
+    import torch
+    engines = {}
+    for m in ("hip", "aql"):
+        engines[m] = _engine(dispatch=m, seed=3)
+        engines[m].run_steps(50)
+        engines[m].synchronize()
+    ns = [1, 2, 5, 10, 20, 50, 200]
+    res = {m: {} for m in engines}
+    for _ in range(15):
+        for m, e in engines.items():
+            for n in ns:
+                e.run_steps(10)   # priming, untimed
+                e.synchronize()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                e.run_steps(n)
+                t1 = time.perf_counter()
+                e.synchronize()
+                ts = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                e.synchronize()          # both again, idle: the bracket's own host cost
+                ti = time.perf_counter()
+                torch.cuda.synchronize()
+                tj = time.perf_counter()
+                res[m].setdefault(n, []).append(((t2 - t0) * 1e6, (t1 - t0) * 1e6, (ts - t1) * 1e6,
+                                                 (t2 - ts) * 1e6, (ti - t2) * 1e6, (tj - ti) * 1e6))
+    for m in engines:
+        tot = [np.median([x[0] for x in res[m][n]]) for n in ns]
+        enq = [np.median([x[1] for x in res[m][n]]) for n in ns]
+        slope, icpt = np.polyfit(ns, tot, 1)
+        print(f"{m}: " + "  ".join(f"n={n}: {t:.1f} us (enq {q:.1f})" for n, t, q in zip(ns, tot, enq)) +
+              f"  | fit: {slope:.2f} us/step + {icpt:.1f} us per batch; n=20 -> {tot[ns.index(20)] / 20:.2f} us/step")
+        for n in (1, 20):
+            med = np.median(np.array(res[m][n]), axis=0)
+            print(f"  {m} n={n}: run_steps call {med[1]:.1f}, engine sync {med[2]:.1f}, torch sync {med[3]:.1f} us; "
+                  f"idle: engine sync {med[4]:.1f}, torch sync {med[5]:.1f} us")
+
+
+def probe_fences():
+    """Native dispatch under MPPI_AQL_FENCES (diagnostic packet fence scopes)."""
+    h, a = _engine(dispatch="hip", seed=3), _engine(dispatch="aql", seed=3)
+    for e in (h, a):
+        e.run_steps(300)
+        e.synchronize()
+    ok = np.array_equal(h.get_u_prev(), a.get_u_prev()) and np.array_equal(h.get_costs(), a.get_costs())
+    rates = []
+    for _ in range(5):
+        a.run_steps(50)
+        a.synchronize()
+        t0 = time.perf_counter()
+        a.run_steps(1000)
+        a.synchronize()
+        rates.append((time.perf_counter() - t0) / 1000 * 1e6)
+    print(f"fences={os.environ.get('MPPI_AQL_FENCES', 'default 0000')} bit-exact vs HIP after 300 steps: {ok}  "
+          f"us/step (1000-step batches): median {np.median(rates):.2f}  all {[round(x, 2) for x in rates]}")
+
+
+def probe_calls(modes="hip,aql"):
+    """Engine.step latency at C3 with a changing state, modes interleaved in blocks of 200."""
+    import torch  # noqa: F401  (the bench's process shape)
+    modes = modes.split(",")
+    eng = {m: _engine(dispatch=m, seed=3) for m in modes}
+    st0 = np.array(STATES["arm"], np.float64)
+    rng = np.random.default_rng(0)
+    lat = {m: [] for m in modes}
+    for _ in range(10):
+        for m, e in eng.items():
+            for i in range(220):
+                st = st0.copy()
+                st[7:14] += rng.normal(0, 0.01, 7)
+                t0 = time.perf_counter()
+                e.step(st)
+                if i >= 20:
+                    lat[m].append((time.perf_counter() - t0) * 1e6)
+    for m in modes:
+        x = np.array(lat[m])
+        print(f"{m}: calls {eng[m].dispatch_info()!r}  p50 {np.median(x):.2f} us  p10 {np.percentile(x, 10):.2f}  "
+              f"p90 {np.percentile(x, 90):.2f}  p99 {np.percentile(x, 99):.2f}")
+
+
+def probe_sequence():
+    """What a (rollout, X) pair costs for X = an empty kernel, a one-block rollout, the finalize."""
+    names = ["rollout+empty", "rollout+rollout(1 block)", "rollout+finalize", "empty", "rollout(1 block)", "rollout"]
+    for model, K, H in (("arm", 4096, 32), ("wholebody", 8192, 64)):
+        e = _engine(model, K, H)
+        e.run_steps(100)
+        e.synchronize()
+        fn = e._L.mppi_probe_sequence
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double)]
+        res = {}
+        for _ in range(5):
+            for m in range(6):
+                us = C.c_double()
+                fn(e._h, 200, m, C.byref(us))
+                res.setdefault(m, []).append(us.value)
+        print(model, K, H, "  ".join(f"{names[m]} {np.median(v):.2f}" for m, v in res.items()), flush=True)
+        e.close()
+
+
+def probe_stamps(model, K, H, bt="0", nb="0"):
+    """Raw stamps of the last rollout launch: s_memtime and s_memrealtime at each wave's start and
+    end give the shader clock, the wave lifetimes and the grid timeline (ramp, body, drain)."""
+    K, H, bt, nb = int(K), int(H), int(bt), int(nb)
+    e = _engine(model, K, H, block_threads=bt, blocks_per_vehicle=nb)
+    for _ in range(30):
+        e.step(np.array(STATES[model], np.float64))
+    print(model, K, H, "block_threads", bt or "default", "nb", nb or "auto", flush=True)
+    fn = e._L.mppi_debug_stamps
+    fn.restype = C.c_int64
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    buf = np.zeros((1 << 20, 16), np.uint64)
+    n = fn(e._h, buf.ctypes.data, buf.shape[0])
+    if n > 0:
+        x = buf[:n].astype(np.int64)
+        clk = x[:, 7] - x[:, 0]                 # shader clock ticks, STAMP(0) .. STAMP(7)
+        rt0, rt1 = x[:, 13], x[:, 14]
+        life_ns = (rt1 - rt0) * 10.0
+        ok = life_ns > 0
+        ghz = np.median(clk[ok] / life_ns[ok])
+        t0 = rt0.min()
+        start_ns, end_ns = (rt0 - t0) * 10.0, (rt1 - t0) * 10.0
+        span = end_ns.max()
+        print(f"waves {n}: shader clock {ghz:.2f} GHz; grid span {span / 1e3:.2f} us; wave life "
+              f"median {np.median(life_ns) / 1e3:.2f} us (p10 {np.percentile(life_ns, 10) / 1e3:.2f}, "
+              f"p90 {np.percentile(life_ns, 90) / 1e3:.2f}); last wave start {start_ns.max() / 1e3:.2f} us, "
+              f"first wave end {end_ns.min() / 1e3:.2f} us")
+        edges = np.linspace(0, span, 21)
+        act = [int(((start_ns <= t) & (end_ns > t)).sum()) for t in edges[:-1] + (edges[1] - edges[0]) / 2]
+        print("waves resident per 5% of the span:", act, flush=True)
+        hw = x[:, 15] & 0xFFFFFFFF
+        xcc = (x[:, 15] >> 32) & 0xF
+        cu, se, simd = (hw >> 8) & 0xF, (hw >> 13) & 0x7, (hw >> 4) & 0x3
+        for c in range(int(xcc.max()) + 1):
+            m = xcc == c
+            if m.any():
+                print(f"  xcc {c}: waves {int(m.sum()):5d}  life median {np.median(life_ns[m]) / 1e3:6.2f} us  "
+                      f"end max {end_ns[m].max() / 1e3:6.2f} us  end median {np.median(end_ns[m]) / 1e3:6.2f} us")
+        key = (xcc * 8 + se) * 16 + cu
+        u, cnt = np.unique(key, return_counts=True)
+        per_cu_end = np.array([end_ns[key == k].max() for k in u])
+        print(f"  CUs used {len(u)}; waves per CU min {cnt.min()} max {cnt.max()}; per-CU last end "
+              f"p10 {np.percentile(per_cu_end, 10) / 1e3:.2f} p50 {np.median(per_cu_end) / 1e3:.2f} "
+              f"max {per_cu_end.max() / 1e3:.2f} us; simd ids {np.bincount(simd).tolist()}", flush=True)
+    e.close()
+
+
+def probe_latency(model="arm", K="4096", H="32"):
+    """Host-inclusive control-call latency: enqueue (set_state + rollout + finalize) vs wait
+    (read_outputs), for the completion-flag poll (default) and MPPI_EVENT_WAIT=1."""
+    K, H = int(K), int(H)
+    state = np.array(STATES[model], np.float64)
+    n = 400
+    for mode in ("flag", "event"):
+        if mode == "event":
+            os.environ["MPPI_EVENT_WAIT"] = "1"
+        else:
+            os.environ.pop("MPPI_EVENT_WAIT", None)
+        e = _engine(model, K, H)
+        for _ in range(50):
+            e.step(state)
+        full, enq, wait = [], [], []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            e.step(state)
+            full.append(time.perf_counter() - t0)
+        for _ in range(n):
+            t0 = time.perf_counter()
+            e.set_state(state)
+            e.rollout()
+            e.finalize()
+            t1 = time.perf_counter()
+            e.read_outputs()
+            t2 = time.perf_counter()
+            enq.append(t1 - t0)
+            wait.append(t2 - t1)
+        q = lambda x, p: np.percentile(np.array(x) * 1e6, p)  # noqa: E731
+        print(f"{model} K={K} H={H} wait={mode}: step p50 {q(full, 50):6.1f} us p99 {q(full, 99):6.1f} | split: "
+              f"enqueue p50 {q(enq, 50):5.1f} us, read_outputs p50 {q(wait, 50):5.1f} us", flush=True)
+        e.close()
+
+
+PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
+          "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency}
+
+if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1] not in PROBES:
+        sys.exit(__doc__)
+    PROBES[sys.argv[1]](*sys.argv[2:])
