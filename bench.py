@@ -64,9 +64,14 @@ WORKLOADS = {
                      desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
     # the N=8 rank's whole step on one GPU: the C4 shard through the engine-owned RCCL
     # communicator with one rank (rollout -> PACK -> ncclAllReduce -> finalize from C)
-    "c4_shard_native1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True,
+    "c4_shard_native1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True, mode="rccl",
                              desc="Whole-body 8192 samples H=64 through a 1-rank RCCL communicator "
                                   "(the N=8 rank's step of BASELINE configs[3])"),
+    # the same rank step through the peer exchange (no collective: finalize blocks exchange their
+    # partials through the ranks' exchange regions; one rank exchanges with itself)
+    "c4_shard_peer1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True, mode="peer",
+                           desc="Whole-body 8192 samples H=64 through the 1-rank peer exchange "
+                                "(the N=8 rank's step of BASELINE configs[3])"),
 }
 
 # the CPU baseline's shapes (C4 K-reduced: the full C4 on CPU is impractical)
@@ -280,6 +285,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     w.pop("desc")
     strong = w.pop("strong", False)
     force_native = w.pop("native", None)
+    mode = w.pop("mode", None)
     if strong:
         if w["n_samples"] % world:
             raise SystemExit(f"{name}: K={w['n_samples']} does not split over {world} ranks")
@@ -287,7 +293,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     V = w.get("n_vehicles", 1)
     native = force_native if force_native is not None else (
         None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False)
-    se = ShardedEngine(seed=1234, native=native, **w)
+    se = ShardedEngine(seed=1234, native=native, mode=mode, **w)
     eng = se.engine
     set_targets(eng, w["model"], V)
     if w["model"] == "quadrotor":   # warm start at hover thrust (quadrotor_mppi.MPPI does the same)
@@ -319,7 +325,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
                "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
                          f"median of 7 batches, on the engine stream",
                "rollout_us_batches": [round(x, 3) for x in rs]}
-        if se.native:   # the step's one collective alone (a collective call on every rank)
+        if se.mode == "rccl":   # the step's one collective alone (a collective call on every rank)
             tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
         se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
         barrier()
@@ -346,11 +352,11 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     out, u0, st = eng.read_outputs()
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
-    comm = eng.comm_info() if se.native else None
+    comm = eng.comm_info() if se.mode == "rccl" else None
     res = {"batches_s": bt, "enqueue_s": benq, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
            "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
-           "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native,
+           "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native, "exchange": se.mode,
            "native_error": se.native_error, "world": world,
            "backend": dist.get_backend() if dist is not None else None,
            "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None}
@@ -426,6 +432,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         if measured:
             rf.update({"peak_measured": measured, "frac_of_measured_fill": rf["achieved"] / measured["fill_GBps"]})
     w = WORKLOADS[workload]
+    r.setdefault("exchange", "rccl" if r["native"] else "torch")
     line = {
         "metric": "MPPI rollouts/sec (K x H state-steps) + control-step p50 latency, K=4096 H=32",
         "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps,
@@ -437,8 +444,9 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                    "samples_total": world * K * V if not r["strong"] else w["n_samples"], "samples_per_gpu": K,
                    "horizon": H, "action_dim": r["A"], "vehicles_per_gpu": V,
                    "noise": "device Philox4x32-10 (+2x32)", "state_dtype": "f64" if r["state_f64"] else "f32",
-                   "parallelism": (f"samples sharded over {world} GPUs, 1 all-reduce/step" if world > 1
-                                   else "1 GPU")},
+                   "parallelism": ((f"samples sharded over {world} GPUs, " +
+                                    ("peer exchange in the finalize/step" if r["exchange"] == "peer"
+                                     else "1 all-reduce/step")) if world > 1 else "1 GPU")},
         "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
                    "enqueue_ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r.get("enqueue_s", [])],
@@ -458,10 +466,14 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         line["multi_gpu"] = {
             "world_size": world, "backend": r["backend"],
             "rccl_nranks": r["rccl_nranks"], "rccl_rank": r["rccl_rank"],
-            "rccl_nranks_source": "ncclCommCount of the engine's communicator" if r["native"] else
+            "rccl_nranks_source": "ncclCommCount of the engine's communicator" if r["exchange"] == "rccl" else
                                   "no RCCL communicator in this run",
-            "collective": ("engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded partial-record slots"
-                           if r["native"] else f"torch.distributed ({r['backend']}) all_reduce(SUM) of the slots"),
+            "exchange": r["exchange"],
+            "collective": {"peer": "none: peer exchange (finalize blocks store tagged partials into every rank's "
+                                   "IPC-mapped exchange region over xGMI and combine them from their own)",
+                           "rccl": "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded "
+                                   "partial-record slots",
+                           "torch": f"torch.distributed ({r['backend']}) all_reduce(SUM) of the slots"}[r["exchange"]],
             "allreduce_us": tim.get("allreduce_us") if tim else None,
             "native_comm_error": r["native_error"],
             "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
@@ -479,7 +491,8 @@ def secondary_entry(s, ns):
          "roofline_frac": rf["frac"], "roofline_frac_back_to_back": rf["frac_back_to_back"],
          "roofline_frac_step": rf["frac_step"]}
     if s["native"]:
-        e.update({"allreduce_us": s["tim"].get("allreduce_us"), "rccl_nranks": s["rccl_nranks"]})
+        e.update({"exchange": s.get("exchange", "rccl"), "allreduce_us": s["tim"].get("allreduce_us"),
+                  "rccl_nranks": s["rccl_nranks"]})
     return e
 
 
@@ -527,7 +540,7 @@ def main():
                          "control steps); no roofline in the line")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="leave the process's CPU affinity alone (default: bind to the GPU's local CPUs)")
-    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4,fleet_c5,quadrotor_c2",
+    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4_shard_peer1,c4,fleet_c5,quadrotor_c2",
                     help="extra workloads reported (N=1 only), comma separated; '' for none")
     args = ap.parse_args()
     # the JSON line is the only thing on stdout: keep the real stdout for it and send fd 1 to

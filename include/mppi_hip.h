@@ -43,6 +43,7 @@ extern "C" {
 
 #define MPPI_ABI_VERSION 6
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
+#define MPPI_PEER_HANDLE_BYTES 64  /* hipIpcMemHandle_t */
 #define MPPI_MAX_ACTION 16
 #define MPPI_MAX_JOINTS 16
 #define MPPI_MAX_HORIZON 256
@@ -242,6 +243,26 @@ mppi_status mppi_comm_init_ex(mppi_engine* e, const uint8_t id[MPPI_COMM_ID_BYTE
 /* The communicator's own rank count and rank (ncclCommCount / ncclCommUserRank). */
 mppi_status mppi_comm_info(mppi_engine* e, int32_t* nranks, int32_t* rank);
 mppi_status mppi_exchange(mppi_engine* e);
+
+/* Peer exchange: the sharded step without a collective (replaces the pack ->
+ * all-reduce -> combine above for one-vehicle shards, at most 8 ranks).  Each rank's engine
+ * opens an exchange region in its own GPU memory (uncached, 2 x ranks x finalize blocks x 68
+ * words of 8 B) and exports it (mppi_peer_open -> an IPC handle); the caller all-gathers the
+ * handles (torch.distributed) and every rank maps the others' regions (mppi_peer_connect, the
+ * handles in rank order).  From then on each finalize block stores its partial -- (rho, eta,
+ * eta2, nan) and its window of N[t], every 8 B word tagged with the step -- into every other
+ * rank's region over xGMI, and combines the ranks' partials (its own from registers, the others
+ * from its own region once all their tags are the step's): a control step is the unsharded step's two kernels (native dispatch included),
+ * no PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
+ * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer finalises
+ * with the nan flag set (stats nonfinite = 2), so a rank that stopped cannot hang the others.
+ * Not combinable with mppi_comm_init / mppi_bind_exchange on the same engine. */
+mppi_status mppi_peer_open(mppi_engine* e, uint8_t handle[MPPI_PEER_HANDLE_BYTES]);
+mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles /* shard_count x MPPI_PEER_HANDLE_BYTES */);
+/* Connection check (collective, before the first step): every rank calls phase 0 (a pattern word
+ * into its slot of every rank's region), then, after a barrier, phase 1 (this rank's region holds
+ * every rank's word: MPPI_OK, else MPPI_ERR_COMM; the region is cleared either way). */
+mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles
  *   DRONE: x_des(3) v_des(3);  ARM: qdes(nq) vdes(nq);  WHOLEBODY: x(3) v(3) qdes(nq) vdes(nq)

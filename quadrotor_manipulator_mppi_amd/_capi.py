@@ -23,6 +23,7 @@ OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
 ABI_VERSION = 6
 COMM_ID_BYTES = 128
+PEER_HANDLE_BYTES = 64
 
 
 class Joint(C.Structure):
@@ -99,6 +100,9 @@ PROTOTYPES = {
     "mppi_comm_available": (_ST, []),
     "mppi_comm_init": (_ST, [_P, C.POINTER(C.c_uint8)]),
     "mppi_comm_init_ex": (_ST, [_P, C.POINTER(C.c_uint8), C.c_int32]),
+    "mppi_peer_open": (_ST, [_P, C.POINTER(C.c_uint8)]),
+    "mppi_peer_connect": (_ST, [_P, C.POINTER(C.c_uint8)]),
+    "mppi_peer_probe": (_ST, [_P, C.c_int32]),
     "mppi_comm_info": (_ST, [_P, _I32, _I32]),
     "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),

@@ -355,6 +355,11 @@ struct mppi_engine {
     float* d_exchange = nullptr;
     ncclComm_t comm = nullptr;          // engine-owned RCCL communicator (mppi_comm_init)
     float* d_xown = nullptr;            // its exchange buffer (shard_count * V * P floats)
+    bool peer = false;                  // peer exchange connected (mppi_peer_connect): no PACK, no collective
+    unsigned long long* d_xregion = nullptr;   // this rank's exchange region (uncached device memory)
+    size_t x_bytes = 0;
+    std::vector<void*> x_opened;        // the other ranks' regions, IPC-mapped
+    unsigned long long** d_xpeers = nullptr;   // (shard_count) region pointers, device resident
     VehicleConst* h_vc = nullptr;       // pinned staging
     unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
     unsigned char* h_out_dev = nullptr; // device view of h_out
@@ -390,8 +395,9 @@ struct mppi_engine {
 namespace {
 
 // the step goes through the exchange slots: several shards, or an engine-owned
-// communicator (a one-rank communicator runs the same pack -> all-reduce -> combine)
-bool sharded(const mppi_engine* e) { return e->cfg.shard_count > 1 || e->comm; }
+// communicator (a one-rank communicator runs the same pack -> all-reduce -> combine).  A shard
+// connected by the peer exchange steps like an unsharded engine: its finalize does the exchange.
+bool sharded(const mppi_engine* e) { return (e->cfg.shard_count > 1 || e->comm) && !e->peer; }
 
 FinTail tail_of(const FinParams& f, int32_t mode) {
     FinTail t;
@@ -402,6 +408,7 @@ FinTail tail_of(const FinParams& f, int32_t mode) {
     t.u_prev = f.u_prev; t.vc = f.vc;
     t.out = f.out; t.u0 = f.u0; t.stats = f.stats; t.flags = f.flags; t.wraw = f.wraw; t.wsmooth = f.wsmooth;
     t.dst = f.dst; t.xbase = f.xbase; t.xslot = f.xslot; t.nslots = f.nslots; t.myslot = f.myslot; t.P = f.P;
+    t.xpeers = f.xpeers; t.xlocal = f.xlocal; t.xn = f.xn; t.xme = f.xme;
     std::memcpy(t.sg, f.sg, sizeof(t.sg));
     return t;
 }
@@ -1058,7 +1065,8 @@ void mppi_destroy(mppi_engine* e) {
     for (auto& pr : e->fin_pairs) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->comm) rccl().destroy(e->comm);
-    void* dev[] = {e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
+    for (void* q : e->x_opened) if (q) (void)hipIpcCloseMemHandle(q);
+    void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
                    e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
     for (void* p : dev) if (p) (void)hipFree(p);
@@ -1258,6 +1266,101 @@ mppi_status mppi_exchange(mppi_engine* e) {
         if (timed_out) return fail(MPPI_ERR_COMM, "ncclAllReduce: not enqueued after %d ms", init_timeout_ms());
     }
     if (rc != ncclSuccess) return fail(MPPI_ERR_COMM, "ncclAllReduce: %s", rccl().err(rc));
+    return MPPI_OK;
+}
+
+// ---------------------------------------------------------------- peer exchange
+// The finalize's grid.x (mppi_launch_finalize: 8 XCD lanes x dim groups x t-slices)
+static size_t fin_blocks(const mppi_engine* e) { return (size_t)8 * ((e->A + 7) / 8) * e->fin_ts * e->V; }
+
+mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
+    if (!e || !handle) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (e->V != 1) return fail(MPPI_ERR_STATE, "peer exchange: one vehicle per engine (V = %d)", e->V);
+    if (e->cfg.shard_count > kMaxPeers)
+        return fail(MPPI_ERR_STATE, "peer exchange: at most %d ranks (%d)", kMaxPeers, e->cfg.shard_count);
+    if (e->comm || e->d_exchange) return fail(MPPI_ERR_STATE, "peer exchange: the engine already has an exchange");
+    if (e->d_xregion) return fail(MPPI_ERR_STATE, "peer exchange: region already open");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const size_t bytes = 2 * (size_t)e->cfg.shard_count * fin_blocks(e) * kXW * sizeof(unsigned long long);
+    // uncached: the words other GPUs store into it are never behind a stale line of this GPU's L2
+    void* p = nullptr;
+    hipError_t r = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+    if (r != hipSuccess) {
+        (void)hipGetLastError();
+        HIP_TRY(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+    }
+    e->d_xregion = (unsigned long long*)p;
+    e->x_bytes = bytes;
+    HIP_TRY(hipMemset(p, 0, bytes));   // tags 0: no step's (bit 31 is set in every tag)
+    hipIpcMemHandle_t h;
+    static_assert(sizeof(h) == MPPI_PEER_HANDLE_BYTES, "hipIpcMemHandle_t size");
+    HIP_TRY(hipIpcGetMemHandle(&h, p));
+    std::memcpy(handle, &h, sizeof(h));
+    return MPPI_OK;
+}
+
+mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles) {
+    if (!e || !handles) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_connect before mppi_peer_open");
+    if (e->peer) return fail(MPPI_ERR_STATE, "peer exchange already connected");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
+    std::vector<unsigned long long*> ptrs(n, nullptr);
+    e->x_opened.assign(n, nullptr);
+    for (int r = 0; r < n; ++r) {
+        if (r == me) { ptrs[r] = e->d_xregion; continue; }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)r * MPPI_PEER_HANDLE_BYTES, sizeof(h));
+        void* q = nullptr;
+        const hipError_t rc = hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess);
+        if (rc != hipSuccess) {
+            for (void*& o : e->x_opened) if (o) { (void)hipIpcCloseMemHandle(o); o = nullptr; }
+            return fail(MPPI_ERR_HIP, "peer exchange: opening rank %d's region: %s", r, hipGetErrorString(rc));
+        }
+        e->x_opened[r] = q;
+        ptrs[r] = (unsigned long long*)q;
+    }
+    if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
+    HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
+    FinParams& f = e->fp;
+    f.xpeers = e->d_xpeers; f.xlocal = e->d_xregion; f.xn = n; f.xme = me;
+    FinTail t[2] = {tail_of(f, 0), tail_of(f, 2)};
+    t[0].wraw = t[0].wsmooth = nullptr;   // (as at create: the step's FINAL stores no readback copies)
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(e->d_tail + kTailFinal, &t[0], sizeof(FinTail), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_tail + kTailReadback, &t[1], sizeof(FinTail), hipMemcpyHostToDevice));
+    e->peer = true;
+    e->call_cached = false;
+    return MPPI_OK;
+}
+
+// Connection check before the first step (distributed.py): phase 0 stores a pattern word into
+// this rank's slot of every rank's region (the same mapping the kernels store through); after a
+// barrier, phase 1 checks that this rank's region holds every rank's pattern and clears it.
+mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->peer) return fail(MPPI_ERR_STATE, "mppi_peer_probe before mppi_peer_connect");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
+    const size_t slot = fin_blocks(e) * kXW;   // words per (parity, rank)
+    auto pattern = [](int r, int d) { return (0x5A5A0000ull | (unsigned)(16 * r + d)) << 32 | 0x3F800000ull; };
+    if (phase == 0) {
+        std::vector<unsigned long long*> ptrs(n);
+        HIP_TRY(hipMemcpy(ptrs.data(), e->d_xpeers, n * sizeof(void*), hipMemcpyDeviceToHost));
+        for (int d = 0; d < n; ++d) {
+            const unsigned long long w = pattern(me, d);
+            HIP_TRY(hipMemcpy(ptrs[d] + (size_t)me * slot, &w, sizeof(w), hipMemcpyHostToDevice));
+        }
+        return MPPI_OK;
+    }
+    std::vector<unsigned long long> got(n);
+    for (int r = 0; r < n; ++r)
+        HIP_TRY(hipMemcpy(&got[r], e->d_xregion + (size_t)r * slot, sizeof(got[r]), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
+    HIP_TRY(hipDeviceSynchronize());
+    for (int r = 0; r < n; ++r)
+        if (got[r] != pattern(r, me))
+            return fail(MPPI_ERR_COMM, "peer exchange: rank %d's probe word did not arrive (%016llx)", r, got[r]);
     return MPPI_OK;
 }
 

@@ -1,6 +1,7 @@
 // mppi_dev.h -- structures shared by the host C-ABI (mppi_capi.cpp) and the
 // gfx950 kernels (mppi_kernels.hip).  Internal: not part of the public ABI.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/mppi_hip.h"
@@ -141,12 +142,29 @@ struct FinTail {
     float* xbase;
     int64_t xslot;
     int32_t nslots, myslot, P, pad_;
+    unsigned long long* const* xpeers;   // peer exchange (mppi_peer_connect): every rank's region, null = off
+    unsigned long long* xlocal;          //   this rank's region (the ranks' partials are gathered from it)
+    int32_t xn, xme;                     //   rank count, this rank
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
 // timing, probes), READBACK (mppi_get_weighted_noise: w_eps and its SavGol of the records as they
 // stand, nothing else written)
 enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTailSlots = 4 };
+
+// Peer exchange of a sharded V == 1 engine (mppi_capi.cpp mppi_peer_open / mppi_peer_connect):
+// every k_finalize block pushes its partial -- header (rho, eta, eta2, nan) and its window's
+// columns N[t] -- into every rank's exchange region, and gathers the ranks' partials of the same
+// block from its own.  Each word is 8 B, (value bits, tag): one store carries its own validity,
+// so nothing is ordered against anything else.  Region: [2 step parities][ranks][V*grid.x blocks]
+// [kXW words].  The tag is the step's Philox counter with bit 31 set, which the rollout's block 0
+// hands to the finalize in the vehicle constants (word kVcStepWord).
+constexpr int kMaxPeers = 8;
+constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
+constexpr int kVcStepWord = (int)(offsetof(VehicleConst, _pad) / 4) + 1;
+// a finalize block waits at most this long for its peers' partials (s_memrealtime, 100 MHz), then
+// finalises with the nan flag set (2): a rank that stopped stepping cannot hang the others
+constexpr uint64_t kPeerWaitTicks = 200000000ull;   // 2 s
 // k_finalize's sequence argument: this value = take the step's sequence number from the vehicle
 // constants (VehicleConst::_pad[0]; native control calls, mppi_aql.cpp).  HIP-path sequence
 // numbers stay below 2^31, native ones have bit 31 set: the two never meet in the flags.
@@ -185,6 +203,9 @@ struct FinParams {
     float* xbase;            // pack: exchange buffer base; the other shards' slots are zeroed at
     int64_t xslot;           //   the same positions (slot stride xslot floats), so the SUM
     int32_t nslots, myslot;  //   all-reduce needs no memset first
+    unsigned long long* const* xpeers;   // peer exchange (FinTail): the ranks' regions, this rank's,
+    unsigned long long* xlocal;          //   rank count, this rank; xpeers null = off
+    int32_t xn, xme;
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

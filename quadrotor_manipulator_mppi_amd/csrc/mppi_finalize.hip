@@ -146,6 +146,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     double* outp = nullptr;
     uint32_t* flags = nullptr;
     const VehicleConst* vcb = nullptr;
+    unsigned long long* const* xpeers = nullptr;   // peer exchange (null: off)
+    unsigned long long* xlocal = nullptr;
+    int32_t xn = 0, xme = 0;
+    uint32_t xstep = 0u;
     float sg[WIN > 0 ? WIN : 1];
     auto pin_tail = [&]() {
         // every load issues first, then two empty asms consume them (one wait): pinned one
@@ -154,13 +158,15 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
         wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
         up = T.u_prev; vcb = T.vc;
+        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme;
         if constexpr (WIN > 0) {
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
         }
         asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
                           "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
-                          "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb));
+                          "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb), "+s"(xpeers), "+s"(xlocal), "+s"(xn),
+                          "+s"(xme));
         if constexpr (WIN == 9)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
                               "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
@@ -177,6 +183,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             x0d = ld_dev(vcp->pos0 + a); v0d = ld_dev(vcp->vel0 + a);
             if (seq == kSeqFromVc) seqv = ld_dev((const uint32_t*)vcp->_pad);   // (its bits)
         }
+        if (tid == 0 && xpeers) xstep = ld_dev((const uint32_t*)(vcb + v) + kVcStepWord);   // the exchange's tag
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
     // column of a row group, so each lane carries them and the wave fold runs over row groups
@@ -279,6 +286,86 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         eta2 = fmaf(f * f, weta2[w], eta2);
     }
     FSTAMP(3);
+    if (xpeers != nullptr && mode != 1) {
+        // Peer exchange (sharded V == 1 engines, mppi_dev.h kXW): this block's partial goes to every
+        // other rank's region (a FINAL only; READBACK re-reads the last step's), then the other
+        // ranks' partials of this block come back from this rank's region, each 8 B word valid once
+        // its tag is this step's, and all are combined in rank order (the same order on every rank: every rank finalises
+        // bit-identically; one rank reproduces the unsharded step exactly, f = exp(0) = 1).
+        const uint32_t step = __builtin_amdgcn_readfirstlane(xstep);
+        const uint32_t tag = step | 0x80000000u;
+        // (the grid from geo, not gridDim: that reads the hidden kernel arguments, which native
+        // dispatch does not supply; V == 1 on a peer-exchange engine)
+        const size_t nbk = (size_t)8 * na * ts, blk = blockIdx.x;
+        const size_t par = step & 1u;
+        const float hown = (lane == 0) ? rho : (lane == 1) ? eta : (lane == 2) ? eta2 : nanf;
+        if (mode == 0) {   // (this rank's own partial stays in registers: no round trip through memory)
+            const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
+            const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
+            const size_t off = ((par * (size_t)xn + (size_t)xme) * nbk + blk) * kXW;
+            for (int d = 0; d < xn; ++d) {
+                if (d == xme) continue;
+                unsigned long long* dst = uniform_ptr(xpeers[d]) + off;
+                if (lane < W) __hip_atomic_store(dst + kHdr + lane, wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (lane < kHdr) __hip_atomic_store(dst + lane, wh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        float nv[kMaxPeers], hv[kMaxPeers];
+#pragma unroll
+        for (int r = 0; r < kMaxPeers; ++r) {
+            nv[r] = (r == xme) ? N : 0.0f;
+            hv[r] = (r == xme) ? hown : 0.0f;
+        }
+        const bool needc = lane < W, needh = lane < kHdr;
+        uint32_t pend = (needc || needh) ? ((1u << xn) - 1u) & ~(1u << xme) : 0u;
+        const unsigned long long* src = xlocal + (par * (size_t)xn * nbk + blk) * kXW;
+        const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+        bool late = false;
+        while (__builtin_amdgcn_ballot_w64(pend != 0u) != 0ull) {
+#pragma unroll
+            for (int r = 0; r < kMaxPeers; ++r) {
+                if (!((pend >> r) & 1u)) continue;
+                const unsigned long long* s = src + (size_t)r * nbk * kXW;
+                bool ok = true;
+                if (needc) {
+                    const unsigned long long x = __hip_atomic_load(s + kHdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = (uint32_t)(x >> 32) == tag;
+                    nv[r] = __uint_as_float((uint32_t)x);
+                }
+                if (needh) {
+                    const unsigned long long y = __hip_atomic_load(s + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = ok && (uint32_t)(y >> 32) == tag;
+                    hv[r] = __uint_as_float((uint32_t)y);
+                }
+                if (ok) pend &= ~(1u << r);
+            }
+            if (__builtin_amdgcn_ballot_w64(pend != 0u) == 0ull) break;
+            if (__builtin_amdgcn_s_memrealtime() - t_in > kPeerWaitTicks) { late = true; break; }   // (2 s)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        rho = INFINITY;
+        nanf = late ? 2.0f : 0.0f;
+#pragma unroll
+        for (int r = 0; r < kMaxPeers; ++r) {
+            if (r < xn) {
+                rho = fminf(rho, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hv[r]), 0)));
+                nanf = fmaxf(nanf, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hv[r]), 3)));
+            }
+        }
+        N = 0.0f; eta = 0.0f; eta2 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < kMaxPeers; ++r) {
+            if (r < xn) {
+                const float rr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hv[r]), 0));
+                const float er = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hv[r]), 1));
+                const float e2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hv[r]), 2));
+                const float f = (rr < INFINITY) ? __expf(coef * (rr - rho)) : 0.0f;
+                N = fmaf(f, nv[r], N);
+                eta = fmaf(f, er, eta);
+                eta2 = fmaf(f * f, e2, eta2);
+            }
+        }
+    }
     const int t = w0 + lane;              // this lane's time index (lanes < W)
     const bool own = lane < W && t >= t_lo && t < t_hi;
     if (mode == 1) {   // PACK raw sums into this shard's exchange slot

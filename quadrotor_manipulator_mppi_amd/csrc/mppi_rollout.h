@@ -738,13 +738,17 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     }
     if (tid < kVCW) {
         ((int*)&vcv)[tid] = vcr;
-        if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize (written through)
-            __hip_atomic_store((int*)pk.vc + tid, vcr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (VONE && blockIdx.x == 0)   // hand vc0 to the finalize (written through), with this
+                                       // step's Philox counter in a spare word (the peer exchange's tag)
+            __hip_atomic_store((int*)pk.vc + tid, tid == kVcStepWord ? (int)step_ctr : vcr, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int i = tid + nthr; i < kVCW; i += nthr) {   // nthr < 124
         const int x = VONE ? ((const int*)&pk.vc0)[i] : ((const int*)(pk.vc + v))[i];
         ((int*)&vcv)[i] = x;
-        if (VONE && blockIdx.x == 0) __hip_atomic_store((int*)pk.vc + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (VONE && blockIdx.x == 0)
+            __hip_atomic_store((int*)pk.vc + i, i == kVcStepWord ? (int)step_ctr : x, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMPW(8);
     if (!(MPPI_KO & 256)) lds_barrier();

@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     if (VONE && b == 0) {   // hand vc0 to the finalize (it reads vc[v])
         constexpr int kVCW = (int)(sizeof(VehicleConst) / 4);
         for (int i = tid; i < kVCW; i += NT)   // (written through: k_rollout's drain_stores)
-            __hip_atomic_store((int*)pk.vc + i, ((const int*)&pk.vc0)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((int*)pk.vc + i, i == kVcStepWord ? (int)step_ctr : ((const int*)&pk.vc0)[i],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (+ the step: mppi_dev.h kVcStepWord)
     }
     // ---- phase 1, all waves: u_prev and the (16 x H) noise tile into LDS.  Noise
     //      (standard_normal_noise.py:22-29 / drone_mppi.py:40-44): the 4 normals of (k, t)

@@ -11,20 +11,26 @@ finalize: rho = min_g rho_g, rescale by exp(-(rho_g - rho)/lambda), SavGol,
 u += w_eps.  The payload is (4 + A*H) floats per vehicle per rank -- 2.6 KB at
 H=64, A=10 -- so the collective is latency-bound; ring bandwidth is irrelevant.
 
-Two ways to run the collective:
+Three ways to run the exchange:
 
-* ``native=True`` (default when the process group is RCCL, backend "nccl"): the
-  engine owns an RCCL communicator (``mppi_comm_init``; rank 0's unique id is
-  broadcast over torch.distributed) and a whole control step -- rollout, pack,
-  all-reduce, finalize -- is enqueued from C with no Python in between
-  (``Engine.run_steps`` / ``Engine.step`` work unchanged on a shard);
+* ``exchange="peer"`` (``native=True`` on a one-vehicle shard; ``MPPI_EXCHANGE=peer``): no
+  collective at all.  Each rank's engine opens an exchange region in its own GPU memory, the ranks
+  all-gather the regions' IPC handles once, and every finalize block stores its partial into every
+  rank's region over xGMI as tagged 8 B words and combines the ranks' partials from its own
+  (``mppi_peer_open`` / ``mppi_peer_connect``, csrc/mppi_finalize.hip).  A step is the unsharded
+  step's two kernels -- native dispatch, no PACK launch, nothing enqueued by the host between
+  them; a connection probe runs before the first step;
+* ``exchange="rccl"`` (``native=True``, the default for ``native`` otherwise): the engine owns an
+  RCCL communicator (``mppi_comm_init``; rank 0's unique id is broadcast over torch.distributed)
+  and a whole control step -- rollout, pack, all-reduce, finalize -- is enqueued from C with no
+  Python in between (``Engine.run_steps`` / ``Engine.step`` work unchanged on a shard);
 * ``native=False``: the engine packs into a torch buffer and ``torch.distributed``
   does the all-reduce (any backend; the gloo tests on CPU and rehearsals use it).
 
-If the native communicator cannot be set up on some rank (no loadable RCCL, a bad
-unique id, peers that do not join before the init deadline), every rank learns it (MIN
-all-reduces of an ok flag, ``setup_native_comm``) and all of them fall back to the
-torch.distributed collective on a fresh engine; ``native_error`` says why.  RCCL's
+If the engine-owned exchange cannot be set up on some rank (no peer mapping, no loadable RCCL, a
+bad unique id, peers that do not join before the init deadline), every rank learns it (MIN
+all-reduces of an ok flag) and all of them take the next way down -- peer, then RCCL, then the
+torch.distributed collective -- on a fresh engine; ``native_error`` says why.  RCCL's
 availability is agreed on before any rank enters the collective init.
 
 The reference has no distributed code (single process, ``CUDA_VISIBLE_DEVICES='0'``
@@ -117,17 +123,70 @@ def combine_slots(slots: np.ndarray, lam: float, H: int, A: int) -> np.ndarray:
     return (N / eta).reshape(A, H).T
 
 
+def setup_peer_exchange(rank: int, world: int, group, device: int, engine: Engine) -> Optional[str]:
+    """Open this rank's exchange region, all-gather the IPC handles, map every rank's region and
+    probe the mapping (``mppi_peer_probe``).  Returns None when every rank is connected, else the
+    reason (the same verdict on every rank)."""
+    def agreed(err):
+        if world > 1 and not _all_ranks_ok(err is None, group, device):
+            return err or "peer exchange failed on another rank"
+        return err
+
+    handle, err = None, None
+    try:
+        handle = engine.peer_open()
+    except Exception as exc:
+        err = str(exc)
+    if (err := agreed(err)) is not None:
+        return err
+    handles = [None] * world
+    if world > 1:
+        dist.all_gather_object(handles, handle, group=group)
+    else:
+        handles = [handle]
+    try:
+        engine.peer_connect(handles)
+        engine.peer_probe(0)
+    except Exception as exc:
+        err = str(exc)
+    if (err := agreed(err)) is not None:
+        return err
+    if world > 1:
+        dist.barrier(group=group)   # every rank's probe words are stored
+    try:
+        engine.peer_probe(1)
+    except Exception as exc:
+        err = str(exc)
+    return agreed(err)
+
+
+def default_exchange(native: bool, world: int, n_vehicles: int) -> str:
+    """MPPI_EXCHANGE (peer | rccl) or, for an engine-owned exchange, peer on one-vehicle shards
+    of at most 8 ranks and RCCL otherwise."""
+    if not native:
+        return "torch"
+    env = os.environ.get("MPPI_EXCHANGE")
+    if env in ("peer", "rccl"):
+        return env
+    return "peer" if n_vehicles == 1 and world <= 8 else "rccl"
+
+
 class ShardedEngine:
     """One rank's engine of a sample-sharded MPPI controller."""
 
     def __init__(self, group=None, exchange: Callable = all_reduce_slots, native: Optional[bool] = None,
-                 **engine_kw):
+                 mode: Optional[str] = None, **engine_kw):
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         if native is None:
             native = self.world > 1 and dist.get_backend(group) == "nccl" and exchange is all_reduce_slots
         self.native = bool(native)
+        # the exchange: "peer" (no collective), "rccl" (engine-owned communicator), "torch"
+        self.mode = mode or default_exchange(self.native, self.world, int(engine_kw.get("n_vehicles", 1) or 1))
+        if self.mode not in ("peer", "rccl", "torch"):
+            raise ValueError(f"exchange mode {self.mode!r}")
+        self.native = self.mode != "torch"
         device = engine_kw.pop("device", 0)
         self.local = int(os.environ.get("LOCAL_RANK", device))
         self.local %= max(1, torch.cuda.device_count())   # more ranks than devices: wrap
@@ -141,18 +200,29 @@ class ShardedEngine:
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
         self.native_error: Optional[str] = None
-        if self.native:   # engine-owned RCCL communicator: the whole step is enqueued from C
+
+        def fresh_engine():
+            self.engine.close()
+            self.engine = Engine(cfg)
+            self.engine.set_stream(self.stream.cuda_stream)
+
+        if self.mode == "peer":
+            err = setup_peer_exchange(self.rank, self.world, group, self.local, self.engine)
+            if err is not None:   # every rank takes the RCCL communicator instead, on a fresh engine
+                self.native_error = f"peer exchange: {err}"
+                self.mode = "rccl"
+                fresh_engine()
+        if self.mode == "rccl":   # engine-owned RCCL communicator: the whole step is enqueued from C
             err = setup_native_comm(self.rank, self.world, group, self.local, Engine.comm_available,
                                     Engine.comm_unique_id, self.engine.comm_init)
             if err is not None and self.world > 1:
                 # a failure on any rank: every rank takes the torch.distributed collective
                 # instead (same slots, same finalize) on a fresh engine, so no rank is left
                 # waiting in a collective alone
-                self.native_error = err
+                self.native_error = (self.native_error + "; " if self.native_error else "") + err
                 self.native = False
-                self.engine.close()
-                self.engine = Engine(cfg)
-                self.engine.set_stream(self.stream.cuda_stream)
+                self.mode = "torch"
+                fresh_engine()
             elif err is not None:
                 raise RuntimeError(err)
         if not self.native and self.world > 1:
@@ -166,7 +236,8 @@ class ShardedEngine:
         """rollout -> (all-reduce) -> finalize, all ordered on self.stream, no host sync."""
         if self.native:
             self.engine.rollout(d_noise_ptr)
-            self.engine.exchange()
+            if self.mode == "rccl":
+                self.engine.exchange()
             self.engine.finalize()
             return
         with torch.cuda.stream(self.stream):
@@ -184,7 +255,7 @@ class ShardedEngine:
                 self.step_async()
 
     def step(self, state, d_noise_ptr: int = 0):
-        if self.world == 1 and not d_noise_ptr:   # one C call, as the drop-in classes step
+        if (self.world == 1 or self.mode == "peer") and not d_noise_ptr:   # one C call, as the drop-in classes step
             return self.engine.step(state)
         self.engine.set_state(state)
         self.step_async(d_noise_ptr)

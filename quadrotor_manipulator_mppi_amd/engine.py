@@ -212,6 +212,24 @@ class Engine:
     def exchange(self):
         capi.check(self._L.mppi_exchange(self._h), "exchange")
 
+    def peer_open(self) -> bytes:
+        """Open this rank's peer-exchange region; returns its IPC handle (mppi_peer_open)."""
+        buf = (C.c_uint8 * capi.PEER_HANDLE_BYTES)()
+        capi.check(self._L.mppi_peer_open(self._h, buf), "peer_open")
+        return bytes(buf)
+
+    def peer_connect(self, handles):
+        """Map every rank's region (handles in rank order, this rank's own included)."""
+        blob = b"".join(bytes(h) for h in handles)
+        if any(len(h) != capi.PEER_HANDLE_BYTES for h in handles):
+            raise ValueError("peer handles must be %d bytes each" % capi.PEER_HANDLE_BYTES)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        capi.check(self._L.mppi_peer_connect(self._h, buf), "peer_connect")
+
+    def peer_probe(self, phase: int):
+        """Connection check (collective): phase 0 on every rank, a barrier, then phase 1."""
+        capi.check(self._L.mppi_peer_probe(self._h, int(phase)), "peer_probe")
+
     def set_stream(self, stream_handle: int):
         capi.check(self._L.mppi_set_stream(self._h, C.c_void_p(stream_handle)), "set_stream")
 

@@ -22,7 +22,7 @@ def _fake_result(world, rank, model="wholebody", K=8192, H=64, native=False, bac
                     "rollout_in_step_us": 12.6 + rank, "method": "fake"},
             "lat": [3e-5] * 10, "K": K, "H": H, "A": 10, "V": 1, "strong": True,
             "bytes": K * H * 88 + 4 * K, "ess": 1.0, "model": model, "state_f64": False, "native": native,
-            "native_error": None, "world": world, "backend": backend,
+            "exchange": "rccl" if native else "torch", "native_error": None, "world": world, "backend": backend,
             "rccl_nranks": world if native else None, "rccl_rank": rank if native else None}
 
 

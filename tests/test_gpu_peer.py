@@ -1,0 +1,193 @@
+"""The peer exchange (mppi_peer_open / mppi_peer_connect, csrc/mppi_finalize.hip): the sharded
+step of SURVEY §8e without a collective.  What is sharded is the reference's softmin and
+weighted sum (``mppi.py:143-148``, ``:184-191``); each finalize block stores its partial into
+every rank's exchange region as tagged 8 B words and combines the ranks' partials from its own.
+
+(a) one rank exchanging with itself reproduces the unsharded engine bit for bit -- native
+    batches, native control calls, HIP launches, and the w_eps readback -- at the C4 shard shape;
+(b) two ranks as two processes on this GPU (gloo only carries the handle all-gather and the
+    probe's barrier), whole-body K = 2 x 4096, H = 64: per-global-k costs bit-identical to one
+    engine over all 8192 samples, both ranks finalise bit-identically, and u0 / u_prev / outputs
+    equal the one-engine step at the north star's rtol 1e-4 (the ranks' partials are combined in
+    another order than the blocks' records);
+(c) a probe word that never arrives fails the connection on every rank.
+More ranks than two do not fit one GPU this way: every finalize block of every rank waits for
+the same block of the others, and one CU holds one finalize block, so 8 ranks' blocks would
+need more CUs than the GPU has (on a node each rank has its own GPU).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+H = 64
+HOME_Q = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]                 # kinova.py:135
+TARGET = ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])   # mppi.py:71-72
+STATE = np.array([0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0] + HOME_Q + [0.0] * 10, np.float64)
+SEED = 0xC4
+
+
+def _engine(**kw):
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    e = Engine(make_config(model="wholebody", n_horizon=H, seed=SEED, **kw))
+    e.set_target(*TARGET)
+    return e
+
+
+def _close(got, want, rtol=0.0, atol=0.0, what=""):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    err = np.abs(got - want)
+    bad = err > atol + rtol * np.abs(want)
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} off, max err {err.max():.3e}"
+
+
+def _connect_self(e):
+    e.peer_connect([e.peer_open()])
+    e.peer_probe(0)
+    e.peer_probe(1)
+
+
+@pytest.mark.parametrize("dispatch", ["aql", "hip"])
+def test_peer_one_rank_equals_unsharded(dispatch, monkeypatch):
+    """(a) at the C4 shard shape (whole-body K=8192 H=64)."""
+    monkeypatch.setenv("MPPI_DISPATCH", dispatch)
+    plain = _engine(n_samples=8192)
+    peer = _engine(n_samples=8192)
+    _connect_self(peer)
+    rng = np.random.default_rng(5)
+    for e in (plain, peer):
+        e.set_state(STATE)
+        e.run_steps(30)
+        e.synchronize()
+    assert np.array_equal(peer.get_u_prev(), plain.get_u_prev()), "u_prev after a 30-step batch"
+    assert np.array_equal(peer.get_costs(), plain.get_costs())
+    if dispatch == "aql":
+        assert peer.dispatch_info().startswith("aql;"), peer.dispatch_info()
+    for i in range(3):
+        st = STATE.copy()
+        st[7:14] += rng.normal(0, 0.02, 7)
+        o1, u1, s1 = plain.step(st)
+        o2, u2, s2 = peer.step(st)
+        assert np.array_equal(o2, o1) and np.array_equal(u2, u1), f"call {i}: outputs"
+        assert (s2[0].rho, s2[0].eta, s2[0].ess) == (s1[0].rho, s1[0].eta, s1[0].ess)
+        assert not s2[0].nonfinite
+    r1, m1 = plain.get_weighted_noise()
+    r2, m2 = peer.get_weighted_noise()
+    assert np.array_equal(r2, r1) and np.array_equal(m2, m1), "w_eps readback through the exchange"
+    assert np.array_equal(peer.get_u_prev(), plain.get_u_prev())
+    peer.close()
+    plain.close()
+
+
+def test_peer_connect_errors():
+    """Misuse is refused: connect before open, a second open, V > 1, an RCCL-bound engine."""
+    from quadrotor_manipulator_mppi_amd import _capi
+    e = _engine(n_samples=1024)
+    with pytest.raises(_capi.MPPIError):
+        e.peer_connect([b"\0" * _capi.PEER_HANDLE_BYTES])
+    h = e.peer_open()
+    with pytest.raises(_capi.MPPIError):
+        e.peer_open()
+    with pytest.raises(ValueError):
+        e.peer_connect([h[:10]])
+    e.close()
+    fleet = _engine(n_samples=1024, n_vehicles=2)
+    with pytest.raises(_capi.MPPIError):
+        fleet.peer_open()
+    fleet.close()
+
+
+def _rank(rank, world, port, k_shard, u_ins, q, skew_probe):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd import distributed as D
+        if skew_probe:
+            if rank == 1:   # (c): this rank's probe words never reach the others
+                real = D.Engine.peer_probe
+                D.Engine.peer_probe = lambda self, phase: None if phase == 0 else real(self, phase)
+            # (two processes on one GPU cannot pair in RCCL: the fallback goes to the torch collective)
+            D.setup_native_comm = lambda *a, **k: "RCCL not tried in this test"
+        se = D.ShardedEngine(mode="peer", model="wholebody", n_samples=k_shard, n_horizon=H, seed=SEED)
+        if skew_probe:
+            q.put((rank, se.mode, se.native_error))
+            return
+        se.engine.set_target(*TARGET)
+        res = []
+        for u_in in u_ins:
+            se.engine.set_u_prev(u_in)
+            out, u0, st = se.step(STATE)
+            res.append((out.copy(), u0.copy(), se.engine.get_u_prev()[0], bool(st[0].nonfinite)))
+        S = se.engine.get_costs()[0]
+        se.engine.set_state(STATE)
+        se.run_steps(40)
+        se.engine.synchronize()
+        q.put((rank, res, se.mode, S, se.engine.get_u_prev()[0], se.engine.dispatch_info()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(world, k_shard, u_ins, skew_probe):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, k_shard, u_ins, q, skew_probe)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+def test_peer_two_ranks_equal_one_engine():
+    """(b) two processes, K = 4096 each, against one engine over K = 8192."""
+    full = _engine(n_samples=8192)
+    steps = []
+    for s in range(2):
+        u_in = full.get_u_prev()[0]
+        out, u0, st = full.step(STATE)
+        steps.append(dict(out=out, u0=u0, S=full.get_costs()[0], u_in=u_in, u_out=full.get_u_prev()[0]))
+    full.close()
+    res = _spawn(2, 4096, [steps[0]["u_in"], steps[1]["u_in"]], False)
+    assert all(r[2] == "peer" for r in res), [r[2] for r in res]
+    S = np.concatenate([r[3] for r in res])
+    assert np.array_equal(S, steps[1]["S"]), "per-global-k costs (step 2)"
+    for s in range(2):
+        out, u0, up, nonfinite = res[0][1][s]
+        assert not nonfinite
+        for a, b in zip(res[1][1][s], res[0][1][s]):
+            assert np.array_equal(a, b), f"step {s}: the ranks finalised differently"
+        _close(u0[0], steps[s]["u0"][0], rtol=1e-4, atol=1e-6, what=f"step {s}: u0")
+        _close(up, steps[s]["u_out"], rtol=1e-4, atol=1e-6, what=f"step {s}: u_prev")
+        tol = 1e-4 * float(np.abs(steps[s]["u0"]).max()) * 0.01 + 1e-9
+        _close(out, steps[s]["out"], atol=tol, what=f"step {s}: outputs")
+    # a 40-step native batch on both ranks: still bit-identical across ranks, finite
+    assert np.array_equal(res[0][4], res[1][4]) and np.isfinite(res[0][4]).all()
+    assert all(r[5].startswith("aql;") for r in res), [r[5] for r in res]
+
+
+def test_peer_probe_failure_falls_back_on_every_rank():
+    """(c) rank 1 skips its probe stores: every rank's connection check fails the same way and
+    every rank moves to the next exchange (RCCL, which then cannot pair two processes on one
+    GPU, so the torch collective) -- no rank is left stepping alone."""
+    res = _spawn(2, 1024, [], True)
+    modes = {r[1] for r in res}
+    assert len(modes) == 1 and "peer" not in modes, modes
+    assert all("peer exchange" in (r[2] or "") for r in res), [r[2] for r in res]
