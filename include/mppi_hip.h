@@ -259,9 +259,11 @@ mppi_status mppi_exchange(mppi_engine* e);
  * Not combinable with mppi_comm_init / mppi_bind_exchange on the same engine. */
 mppi_status mppi_peer_open(mppi_engine* e, uint8_t handle[MPPI_PEER_HANDLE_BYTES]);
 mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles /* shard_count x MPPI_PEER_HANDLE_BYTES */);
-/* Connection check (collective, before the first step): every rank calls phase 0 (a pattern word
- * into its slot of every rank's region), then, after a barrier, phase 1 (this rank's region holds
- * every rank's word: MPPI_OK, else MPPI_ERR_COMM; the region is cleared either way). */
+/* Connection check (collective, before the first step; a barrier between phases): phase 0 copies
+ * a pattern word into this rank's slot of every rank's region; phase 1 checks that this rank's
+ * region holds every rank's word (MPPI_OK, else MPPI_ERR_COMM) and clears it; phase 2 runs the
+ * finalize's own tagged stores and polls over the regions in a one-wave kernel (every rank's word
+ * within 2 s, else MPPI_ERR_COMM) and clears the region again. */
 mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles

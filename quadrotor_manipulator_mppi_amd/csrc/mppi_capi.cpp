@@ -1334,15 +1334,35 @@ mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles) {
     return MPPI_OK;
 }
 
-// Connection check before the first step (distributed.py): phase 0 stores a pattern word into
-// this rank's slot of every rank's region (the same mapping the kernels store through); after a
-// barrier, phase 1 checks that this rank's region holds every rank's pattern and clears it.
+// Connection check before the first step (distributed.py), three phases with a barrier between
+// each: 0 stores a pattern word into this rank's slot of every rank's region through the mapping
+// (a copy); 1 checks that this rank's region holds every rank's word and clears it; 2 runs the
+// finalize's own store-and-poll over the regions in a one-wave kernel (k_peer_probe: every rank's
+// tagged word must arrive within 2 s) and clears the region again.
 mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (!e->peer) return fail(MPPI_ERR_STATE, "mppi_peer_probe before mppi_peer_connect");
     if (use_device(e)) return MPPI_ERR_HIP;
     const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
     const size_t slot = fin_blocks(e) * kXW;   // words per (parity, rank)
+    if (phase == 2) {
+        unsigned long long* d_got = nullptr;
+        HIP_TRY(hipMalloc(&d_got, kMaxPeers * sizeof(unsigned long long)));
+        const uint32_t tag = 0x3C3C0000u;   // (bit 31 clear: never a step's tag)
+        int rc = mppi_launch_peer_probe(e->d_xpeers, e->d_xregion, n, me, slot, tag, kPeerWaitTicks, d_got, e->stream);
+        std::vector<unsigned long long> got(kMaxPeers, 0ull);
+        hipError_t he = rc == 0 ? hipStreamSynchronize(e->stream) : (hipError_t)rc;
+        if (he == hipSuccess) he = hipMemcpy(got.data(), d_got, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+        (void)hipFree(d_got);
+        if (he != hipSuccess) return fail(MPPI_ERR_HIP, "peer probe kernel: %s", hipGetErrorString(he));
+        HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
+        HIP_TRY(hipDeviceSynchronize());
+        for (int r = 0; r < n; ++r)
+            if ((uint32_t)(got[r] >> 32) != (tag | (uint32_t)r))
+                return fail(MPPI_ERR_COMM, "peer exchange: rank %d's word did not reach this rank's region in the "
+                                           "kernel probe (%016llx)", r, got[r]);
+        return MPPI_OK;
+    }
     auto pattern = [](int r, int d) { return (0x5A5A0000ull | (unsigned)(16 * r + d)) << 32 | 0x3F800000ull; };
     if (phase == 0) {
         std::vector<unsigned long long*> ptrs(n);

@@ -231,6 +231,9 @@ int mppi_launch_rollout_arm32(const mppi::DevParams* p, int block_threads, void*
 int mppi_launch_rollout_wb(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_quad(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_finalize(const mppi::FinParams* p, void* stream);
+int mppi_launch_peer_probe(unsigned long long* const* peers, unsigned long long* local, int n, int me,
+                           unsigned long long slot_words, uint32_t tag, unsigned long long ticks,
+                           unsigned long long* out, void* stream);
 int mppi_launch_weights(const float* S, const float* stats, float* w, int V, int K, float coef,
                         void* stream);
 int mppi_launch_philox(uint64_t seed, uint32_t step, int vehicle, int64_t k0, int K, int H, int A,

@@ -505,6 +505,39 @@ extern "C" __global__ void __launch_bounds__(64) k_dispatch_probe(unsigned long 
     if (threadIdx.x == 0) out[0] = mppi_dispatch_id();
 }
 
+// The peer exchange's connection check (mppi_peer_probe phase 2): the finalize's own store and
+// poll instructions over the mapped regions.  Lane d < n stores this rank's tagged word into rank
+// d's region (word 0 of this rank's slot, parity 0), then lane r polls its own region for rank r's
+// word until the tag matches or `ticks` (100 MHz) pass; out[r] = the word seen.
+extern "C" __global__ void __launch_bounds__(64) k_peer_probe(unsigned long long* const* peers,
+                                                              unsigned long long* local, int n, int me,
+                                                              unsigned long long slot_words, uint32_t tag,
+                                                              unsigned long long ticks,
+                                                              unsigned long long* out) {
+    const int lane = threadIdx.x;
+    const unsigned long long w = ((unsigned long long)(tag | (uint32_t)me) << 32) | 0x3F800000ull;
+    if (lane < n) __hip_atomic_store(peers[lane] + (size_t)me * slot_words, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long got = 0ull;
+    if (lane < n) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            got = __hip_atomic_load(local + (size_t)lane * slot_words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((uint32_t)(got >> 32) == (tag | (uint32_t)lane)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        out[lane] = got;
+    }
+}
+
+extern "C" int mppi_launch_peer_probe(unsigned long long* const* peers, unsigned long long* local, int n, int me,
+                                      unsigned long long slot_words, uint32_t tag, unsigned long long ticks,
+                                      unsigned long long* out, void* stream) {
+    hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, peers, local, n, me, slot_words, tag,
+                       ticks, out);
+    return (int)hipGetLastError();
+}
+
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only
 __global__ void k_weights(const float* S, const float* stats, float* w, int V, int K, float coef) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

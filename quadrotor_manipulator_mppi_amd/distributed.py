@@ -151,23 +151,26 @@ def setup_peer_exchange(rank: int, world: int, group, device: int, engine: Engin
         err = str(exc)
     if (err := agreed(err)) is not None:
         return err
-    if world > 1:
-        dist.barrier(group=group)   # every rank's probe words are stored
-    try:
-        engine.peer_probe(1)
-    except Exception as exc:
-        err = str(exc)
-    return agreed(err)
+    for phase in (1, 2):   # 1: the copied words arrived; 2: the finalize's stores and polls
+        if world > 1:
+            dist.barrier(group=group)
+        try:
+            engine.peer_probe(phase)
+        except Exception as exc:
+            err = str(exc)
+        if (err := agreed(err)) is not None:
+            return err
+    return None
 
 
 def default_exchange(native: bool, world: int, n_vehicles: int) -> str:
-    """MPPI_EXCHANGE (peer | rccl) or, for an engine-owned exchange, peer on one-vehicle shards
-    of at most 8 ranks and RCCL otherwise."""
+    """MPPI_EXCHANGE (peer | rccl | torch; also over a gloo group, for rehearsals on one GPU) or,
+    for an engine-owned exchange, peer on one-vehicle shards of at most 8 ranks and RCCL otherwise."""
+    env = os.environ.get("MPPI_EXCHANGE")
+    if env in ("peer", "rccl", "torch"):
+        return env
     if not native:
         return "torch"
-    env = os.environ.get("MPPI_EXCHANGE")
-    if env in ("peer", "rccl"):
-        return env
     return "peer" if n_vehicles == 1 and world <= 8 else "rccl"
 
 

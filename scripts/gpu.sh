@@ -12,6 +12,7 @@
 #   scripts/gpu.sh abi      <tag> <lib.so> ..             same-process interleaved A/B, HIP launches
 #   scripts/gpu.sh timeline <tag> <lib.so> <workload> ..  wall-clock step timelines (timeline build)
 #   scripts/gpu.sh probe    <tag> <probe> [args]          one tools/probes.py probe
+#   scripts/gpu.sh peer2    <tag>                         2-rank peer-exchange rehearsal of the N>1 bench path
 #   scripts/gpu.sh pmc      <tag> [bench.py args]         rocprofv3 counter passes, one group per pass
 #   scripts/gpu.sh traffic  <tag> [workload[:K] ...]      FETCH_SIZE / WRITE_SIZE per launch shape ->
 #                                                         gpurun_out/traffic_<tag>/pmc_rollout.json
@@ -66,6 +67,14 @@ ab_both_orders() {   # $1 tool, rest: libs
   rc=$?; echo "== reversed order"; grep -v amdgpu.ids $out/ab2.txt; exit $rc
 }
 
+peer2() {   # the N>1 bench path through the peer exchange, 2 ranks on this one GPU (gloo carries
+            # only the handle all-gather, the probe's barriers and the timing reductions)
+  MPPI_DIST_BACKEND=gloo MPPI_EXCHANGE=peer timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 50 --warmup 10 \
+      --latency-steps 20 > $out/bench_peer2.json 2> $out/bench_peer2.err || fail "peer rehearsal" $? $out/bench_peer2.err
+  python3 -c "import json;d=json.load(open('$out/bench_peer2.json'));m=d['multi_gpu'];print('peer2', d['config']['parallelism'], 'step %.2f us'%(d['ms_per_step']*1e3), m['exchange'], m['native_comm_error'])"
+}
+
 case $cmd in
 tests)
   run_tests $out/gpu_tests.log "$@" ;;
@@ -83,7 +92,10 @@ final)
   MPPI_DIST_BACKEND=gloo MPPI_NATIVE_COMM=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 \
       --latency-steps 20 > $out/bench_gloo2.json 2> $out/bench_gloo2.err || fail "gloo rehearsal" $? $out/bench_gloo2.err
+  peer2
   echo "final done" ;;
+peer2)
+  peer2 ;;
 ab)
   ab_both_orders tools/ab_native.py "$@" ;;
 abi)

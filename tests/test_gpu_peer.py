@@ -50,6 +50,7 @@ def _connect_self(e):
     e.peer_connect([e.peer_open()])
     e.peer_probe(0)
     e.peer_probe(1)
+    e.peer_probe(2)
 
 
 @pytest.mark.parametrize("dispatch", ["aql", "hip"])
