@@ -242,3 +242,80 @@ def test_native_comm_setup_agreement_world2(fault):
         assert all(r[1] for r in res)
         assert "not ready after" in res[1][1]
         assert [r[2] for r in res] == [[128], [128]]
+
+
+class _FakePeerEngine:
+    """The three peer-exchange calls of Engine, recording what the setup hands them."""
+
+    def __init__(self, rank, fault):
+        self.rank, self.fault, self.calls = rank, fault, []
+
+    def peer_open(self):
+        self.calls.append("open")
+        if self.fault == "open" and self.rank == 1:
+            raise RuntimeError("[mppi status -4] peer_open: peer exchange: one vehicle per engine (V = 2)")
+        return bytes([self.rank]) * 64
+
+    def peer_connect(self, handles):
+        self.calls.append(("connect", [h[0] for h in handles]))
+
+    def peer_probe(self, phase):
+        self.calls.append(("probe", phase))
+        if self.fault == "probe" and self.rank == 0 and phase == 2:
+            raise RuntimeError("[mppi status -6] peer_probe: peer exchange: rank 1's word did not reach this "
+                               "rank's region in the kernel probe")
+
+
+def _peer_rank(rank, world, port, q, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd.distributed import setup_peer_exchange
+        e = _FakePeerEngine(rank, fault)
+        err = setup_peer_exchange(rank, world, None, 0, e)
+        q.put((rank, err, e.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault", [None, "open", "probe"])
+def test_peer_exchange_setup_agreement_world2(fault):
+    """distributed.setup_peer_exchange under gloo: every rank receives every rank's handle in
+    rank order, runs the three probe phases in step with the others, and a failure on one rank
+    (a region that cannot be opened, a probe word that never arrives) gives every rank the same
+    verdict at the same phase -- the cue for all of them to take the RCCL path -- instead of a
+    rank that steps alone."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer_rank, args=(r, world, port, q, fault)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = ["open", ("connect", [0, 1]), ("probe", 0), ("probe", 1), ("probe", 2)]
+    if fault is None:
+        assert [r[1] for r in res] == [None, None]
+        assert [r[2] for r in res] == [full, full]
+    elif fault == "open":
+        assert all(r[1] for r in res) and "one vehicle" in res[1][1]
+        assert [r[2] for r in res] == [["open"], ["open"]], "no rank may connect"
+    else:
+        assert all(r[1] for r in res) and "did not reach" in res[0][1]
+        assert [r[2] for r in res] == [full, full]
+
+
+def test_default_exchange(monkeypatch):
+    from quadrotor_manipulator_mppi_amd.distributed import default_exchange
+    monkeypatch.delenv("MPPI_EXCHANGE", raising=False)
+    assert default_exchange(False, 2, 1) == "torch"
+    assert default_exchange(True, 8, 1) == "peer"
+    assert default_exchange(True, 16, 1) == "rccl"
+    assert default_exchange(True, 2, 8) == "rccl"
+    monkeypatch.setenv("MPPI_EXCHANGE", "rccl")
+    assert default_exchange(True, 8, 1) == "rccl"
+    monkeypatch.setenv("MPPI_EXCHANGE", "peer")
+    assert default_exchange(False, 2, 1) == "peer"
