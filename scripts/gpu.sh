@@ -5,8 +5,9 @@
 #   scripts/gpu.sh bench    <tag> [bench.py args]         default bench line + the driver's 20-step shape x2
 #   scripts/gpu.sh prof     <tag> [workload ...]          rocprofv3 kernel traces of control steps only,
 #                                                         beside the unprofiled line of the same workload
-#   scripts/gpu.sh final    <tag>                         the round's evidence: tests, bench lines, rocprof
-#                                                         (bench command + steps-only per workload), gloo x2
+#   scripts/gpu.sh final    <tag>                         the round's evidence: tests, bench lines, rocprof of
+#                                                         the bench command, gloo and peer 2-rank rehearsals
+#                                                         (steps-only traces per workload: `prof`)
 #   scripts/gpu.sh ab       <tag> <lib.so[@ENV=v,..]> ..  same-process A/B of builds, native dispatch,
 #                                                         both library orders ([AB_REPS] [AB_RUNS])
 #   scripts/gpu.sh abi      <tag> <lib.so> ..             same-process interleaved A/B, HIP launches
@@ -88,7 +89,6 @@ final)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $out/prof_bench -o run -- \
       python3 bench.py --steps 500 --warmup 50 --no-cpu-baseline --secondary "" --latency-steps 100 \
       > $out/prof_bench.json 2> $out/prof_bench.err || fail "rocprof bench" $? $out/prof_bench.err
-  for w in arm_c3 wholebody_c4 c4_shard_native1 c4 drone_c2 quadrotor_c2 fleet_c5; do prof_steps $w; done
   MPPI_DIST_BACKEND=gloo MPPI_NATIVE_COMM=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 \
       --latency-steps 20 > $out/bench_gloo2.json 2> $out/bench_gloo2.err || fail "gloo rehearsal" $? $out/bench_gloo2.err
