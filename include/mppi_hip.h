@@ -273,18 +273,19 @@ mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase);
 mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats* stats);
 
 /* One whole control step: set_state, (upload host noise), rollout, finalize, read_outputs.
- * h_noise: host eps (V,K,H,A) in INJECTED mode, else NULL.  Single-shard, or a
- * shard with an engine-owned communicator. */
+ * h_noise: host eps (V,K,H,A) in INJECTED mode, else NULL.  Single-shard, a shard connected
+ * by the peer exchange, or a shard with an engine-owned communicator. */
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out,
                       float* u0, mppi_stats* stats);
 
 /* n back-to-back asynchronous control steps (rollout + finalize each, device
- * noise, state and warm start resident on the GPU); single-shard engines, or
- * shards with an engine-owned communicator (rollout, all-reduce, finalize).
+ * noise, state and warm start resident on the GPU); single-shard engines, shards connected
+ * by the peer exchange, or shards with an engine-owned communicator (rollout, PACK,
+ * all-reduce, finalize).
  * No host synchronisation: pair with mppi_synchronize / mppi_read_outputs.
- * Single-shard engines dispatch the steps natively: raw AQL packets on an HSA queue the
- * engine owns, the kernels from the library's code objects, their arguments resident in
- * device memory (MPPI_DISPATCH = auto (default) | aql (required) | hip). */
+ * Single-shard and peer-exchange engines dispatch the steps natively: raw AQL packets on an
+ * HSA queue the engine owns, the kernels from the library's code objects, their arguments
+ * resident in device memory (MPPI_DISPATCH = auto (default) | aql (required) | hip). */
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 
 /* How the last mppi_run_steps and the last mppi_step were dispatched:
