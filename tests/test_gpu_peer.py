@@ -85,6 +85,47 @@ def test_peer_one_rank_equals_unsharded(dispatch, monkeypatch):
     plain.close()
 
 
+@pytest.mark.parametrize("model,kw,state", [
+    ("arm", dict(n_samples=4096, n_horizon=32, state_f64=True),
+     [0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0] + HOME_Q + [0.0] * 7),
+    ("drone", dict(n_samples=2048, n_horizon=100, savgol_window=31), [0.1, -0.2, 1.0, 0.0, 0.0, 0.0]),
+    ("quadrotor", dict(n_samples=1024, n_horizon=32), [0.0, 0.0, 1.0] + [0.0] * 9),
+])
+def test_peer_one_rank_equals_unsharded_models(model, kw, state):
+    """(a) for the other kernel families and the widest SavGol window (a 38-column finalize
+    window: the exchange's full 64-column word block), native batches and control calls."""
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    st = np.array(state, np.float64)
+    engines = []
+    for _ in range(2):
+        e = Engine(make_config(model=model, seed=SEED, **kw))
+        if model == "drone" or model == "quadrotor":
+            e.set_target([1.0, 2.0, 3.4])
+        else:
+            e.set_target(*TARGET)
+        if model == "quadrotor":
+            u = np.zeros((1, e.H, e.A), np.float32)
+            u[..., 0] = e.cfg.quad_mass * e.cfg.quad_gravity
+            e.set_u_prev(u)
+        e.set_state(st)
+        engines.append(e)
+    plain, peer = engines
+    _connect_self(peer)
+    for e in engines:
+        e.run_steps(25)
+        e.synchronize()
+    assert np.array_equal(peer.get_u_prev(), plain.get_u_prev()), "u_prev after a native batch"
+    for i in range(3):
+        o1, u1, _ = plain.step(st)
+        o2, u2, _ = peer.step(st)
+        assert np.array_equal(o2, o1) and np.array_equal(u2, u1), f"call {i}"
+    r1, m1 = plain.get_weighted_noise()
+    r2, m2 = peer.get_weighted_noise()
+    assert np.array_equal(r2, r1) and np.array_equal(m2, m1)
+    peer.close()
+    plain.close()
+
+
 def test_peer_connect_errors():
     """Misuse is refused: connect before open, a second open, V > 1, an RCCL-bound engine."""
     from quadrotor_manipulator_mppi_amd import _capi
