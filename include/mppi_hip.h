@@ -256,6 +256,11 @@ mppi_status mppi_exchange(mppi_engine* e);
  * no PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
  * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer finalises
  * with the nan flag set (stats nonfinite = 2), so a rank that stopped cannot hang the others.
+ * Every rank must run the same sequence of steps with the same step counter (the tags are the
+ * Philox counter): a rank that skips a step or rewinds its counter alone leaves the others
+ * waiting out the 2 s bound.  mppi_get_weighted_noise gathers the last exchanged step's
+ * partials (after mppi_kernel_timing, which exchanges nothing, it is undefined, as the
+ * records it reads are then the timing launches').
  * Not combinable with mppi_comm_init / mppi_bind_exchange on the same engine. */
 mppi_status mppi_peer_open(mppi_engine* e, uint8_t handle[MPPI_PEER_HANDLE_BYTES]);
 mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles /* shard_count x MPPI_PEER_HANDLE_BYTES */);
