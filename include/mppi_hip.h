@@ -247,13 +247,14 @@ mppi_status mppi_exchange(mppi_engine* e);
 /* Peer exchange: the sharded step without a collective (replaces the pack ->
  * all-reduce -> combine above for one-vehicle shards, at most 8 ranks).  Each rank's engine
  * opens an exchange region in its own GPU memory (uncached, 2 x ranks x finalize blocks x 68
- * words of 8 B) and exports it (mppi_peer_open -> an IPC handle); the caller all-gathers the
- * handles (torch.distributed) and every rank maps the others' regions (mppi_peer_connect, the
- * handles in rank order).  From then on each finalize block stores its partial -- (rho, eta,
- * eta2, nan) and its window of N[t], every 8 B word tagged with the step -- into every other
- * rank's region over xGMI, and combines the ranks' partials (its own from registers, the others
- * from its own region once all their tags are the step's): a control step is the unsharded step's two kernels (native dispatch included),
- * no PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
+ * words of 8 B: 5.6 MB at 8 ranks for the C4 shard) and exports it (mppi_peer_open -> an IPC
+ * handle); the caller all-gathers the handles (torch.distributed) and every rank maps the
+ * others' regions (mppi_peer_connect, the handles in rank order).  From then on each finalize
+ * block stores its partial -- (rho, eta, eta2, nan) and its window of N[t], every 8 B word
+ * tagged with the step -- into every other rank's region over xGMI, and combines the ranks'
+ * partials (its own from registers, the others from its own region once all their tags are the
+ * step's): a control step is the unsharded step's two kernels (native dispatch included), no
+ * PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
  * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer finalises
  * with the nan flag set (stats nonfinite = 2), so a rank that stopped cannot hang the others.
  * Every rank must run the same sequence of steps with the same step counter (the tags are the

@@ -1270,8 +1270,10 @@ mppi_status mppi_exchange(mppi_engine* e) {
 }
 
 // ---------------------------------------------------------------- peer exchange
-// The finalize's grid.x (mppi_launch_finalize: 8 XCD lanes x dim groups x t-slices)
-static size_t fin_blocks(const mppi_engine* e) { return (size_t)8 * ((e->A + 7) / 8) * e->fin_ts * e->V; }
+// An upper bound of the finalize's blocks: its grid.x is 8 XCD lanes x dim groups x t-slices
+// (mppi_launch_finalize), and the dim groups are A / MPPI_FIN_XCDS rounded up, at most A (the
+// kernel indexes the region with its own grid, so any build's fits)
+static size_t fin_blocks(const mppi_engine* e) { return (size_t)8 * e->A * e->fin_ts * e->V; }
 
 mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
     if (!e || !handle) return fail(MPPI_ERR_INVALID_ARG, "null argument");
