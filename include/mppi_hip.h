@@ -158,7 +158,8 @@ typedef struct {
     float rho;          /* min_k S_k                                        */
     float eta;          /* sum_k exp(-(S_k - rho)/lambda)                   */
     float ess;          /* effective sample size 1 / sum_k w_k^2            */
-    int32_t nonfinite;  /* 1 if rho/eta/u is not finite (reference propagates NaN) */
+    int32_t nonfinite;  /* 1 if rho/eta/u is not finite (reference propagates NaN); 2 if a
+                           peer-exchange step gave up waiting for another rank (u_prev kept) */
     int32_t reach;      /* check_reach result (arm / whole-body)            */
     int32_t _pad;
 } mppi_stats;
@@ -255,8 +256,9 @@ mppi_status mppi_exchange(mppi_engine* e);
  * partials (its own from registers, the others from its own region once all their tags are the
  * step's): a control step is the unsharded step's two kernels (native dispatch included), no
  * PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
- * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer finalises
- * with the nan flag set (stats nonfinite = 2), so a rank that stopped cannot hang the others.
+ * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer gives up:
+ * the step keeps the warm start (w_eps = 0) and reports stats nonfinite = 2, so a rank that
+ * stopped cannot hang or poison the others.
  * Every rank must run the same sequence of steps with the same step counter (the tags are the
  * Philox counter): a rank that skips a step or rewinds its counter alone leaves the others
  * waiting out the 2 s bound.  mppi_get_weighted_noise gathers the last exchanged step's

@@ -1632,7 +1632,9 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
                               std::fabs(T16[11] - e->tpos[3 * v + 2]);
             reach = err < e->cfg.reach_tol;
         }
-        const int nf = (st[4 * v + 3] > 0.0f) || !std::isfinite(st[4 * v]) || !std::isfinite(uu[(size_t)v * e->A]);
+        // 2: a peer-exchange step that waited out its bound for another rank (it kept u_prev)
+        const int nf = (st[4 * v + 3] >= 2.0f) ? 2
+                       : ((st[4 * v + 3] > 0.0f) || !std::isfinite(st[4 * v]) || !std::isfinite(uu[(size_t)v * e->A]));
         nonfinite |= nf;
         if (stats) {
             stats[v].rho = st[4 * v];

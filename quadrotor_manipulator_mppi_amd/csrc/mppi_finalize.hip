@@ -286,6 +286,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         eta2 = fmaf(f * f, weta2[w], eta2);
     }
     FSTAMP(3);
+    bool xlate = false;   // the peer exchange timed out: this step keeps the warm start (w_eps = 0)
     if (xpeers != nullptr && mode != 1) {
         // Peer exchange (sharded V == 1 engines, mppi_dev.h kXW): this block's partial goes to every
         // other rank's region (a FINAL only; READBACK re-reads the last step's), then the other
@@ -365,6 +366,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                 eta2 = fmaf(f * f, e2, eta2);
             }
         }
+        if (late) { xlate = true; N = 0.0f; }
     }
     const int t = w0 + lane;              // this lane's time index (lanes < W)
     const bool own = lane < W && t >= t_lo && t < t_hi;
@@ -391,7 +393,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     }
 
     // FINAL: w_eps = N/eta over the window, SavGol, u += w_eps
-    const float etaf = (nanf > 0.0f) ? NAN : eta;
+    const float etaf = xlate ? 1.0f : (nanf > 0.0f) ? NAN : eta;
     const float w = __fdividef(N, etaf);
     FSTAMP(4);
     // SavGol with the reference's symmetric pad (svg_filter.py:58: index -i-1 left of 0,

@@ -225,6 +225,57 @@ def test_peer_two_ranks_equal_one_engine():
     assert all(r[5].startswith("aql;") for r in res), [r[5] for r in res]
 
 
+def _timeout_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import time
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
+        se = ShardedEngine(mode="peer", model="wholebody", n_samples=1024, n_horizon=H, seed=SEED)
+        res = None
+        if rank == 0:   # rank 1 never steps: this rank's finalize gives up after its 2 s bound
+            se.engine.set_target(*TARGET)
+            u_in = (np.arange(H * 10, dtype=np.float32).reshape(1, H, 10) % 7 - 3.0) * 0.01
+            se.engine.set_u_prev(u_in)
+            t0 = time.perf_counter()
+            out, u0, st = se.step(STATE)
+            res = (time.perf_counter() - t0, int(st[0].nonfinite), bool(np.isfinite(out).all()),
+                   bool(np.array_equal(se.engine.get_u_prev(), u_in)), float(u0[0, 0]), float(u_in[0, 0, 0]))
+        dist.barrier()
+        q.put((rank, se.mode, res))
+        se.engine.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_timeout_keeps_warm_start():
+    """A rank whose peer never steps: its finalize blocks wait out the 2 s bound, then the step
+    keeps the warm start (u_prev unchanged, outputs from it, finite) and reports nonfinite = 2."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_timeout_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert [r[1] for r in res] == ["peer", "peer"]
+    dt, nonfinite, finite, kept, u0, u_in0 = res[0][2]
+    assert nonfinite == 2 and finite and kept, res[0][2]
+    assert u0 == u_in0, "u0 is the kept warm start's first step"
+    assert 1.5 < dt < 30.0, dt
+
+
 def test_peer_probe_failure_falls_back_on_every_rank():
     """(c) rank 1 skips its probe stores: every rank's connection check fails the same way and
     every rank moves to the next exchange (RCCL, which then cannot pair two processes on one
