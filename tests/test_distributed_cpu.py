@@ -192,6 +192,12 @@ def test_native_comm_entry_points_reject_bad_arguments():
     r, f, pr = C.c_double(), C.c_double(), C.c_double()
     assert L.mppi_kernel_timing_ex(None, 10, C.byref(r), C.byref(f), C.byref(pr)) == capi.ERR_INVALID_ARG
     assert "bad arguments" in L.mppi_last_error().decode()
+    # the peer exchange's entry points as well
+    h = (C.c_uint8 * capi.PEER_HANDLE_BYTES)()
+    assert L.mppi_peer_open(None, h) == capi.ERR_INVALID_ARG
+    assert L.mppi_peer_connect(None, h) == capi.ERR_INVALID_ARG
+    assert L.mppi_peer_probe(None, 0) == capi.ERR_INVALID_ARG
+    assert "null" in L.mppi_last_error().decode()
 
 
 def _setup_rank(rank, world, port, q, fault):
