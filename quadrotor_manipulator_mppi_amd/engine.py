@@ -29,6 +29,7 @@ class StepStats:
     ess: float
     nonfinite: bool
     reach: bool
+    exchange_timeout: bool = False   # a peer-exchange step gave up waiting for a rank (u_prev kept)
 
 
 def fill_joints(cfg: capi.Config, chain: Sequence[Dict]) -> None:
@@ -304,7 +305,7 @@ class Engine:
 
     def stats(self) -> List[StepStats]:
         st = self._stats
-        return [StepStats(s.rho, s.eta, s.ess, bool(s.nonfinite), bool(s.reach))
+        return [StepStats(s.rho, s.eta, s.ess, bool(s.nonfinite), bool(s.reach), s.nonfinite == 2)
                 for s in ((st[0],) if self.V == 1 else st)]
 
     # -------------------------------------------------------------- exchange

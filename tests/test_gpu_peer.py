@@ -241,7 +241,7 @@ def _timeout_rank(rank, world, port, q):
             se.engine.set_u_prev(u_in)
             t0 = time.perf_counter()
             out, u0, st = se.step(STATE)
-            res = (time.perf_counter() - t0, int(st[0].nonfinite), bool(np.isfinite(out).all()),
+            res = (time.perf_counter() - t0, (st[0].nonfinite, st[0].exchange_timeout), bool(np.isfinite(out).all()),
                    bool(np.array_equal(se.engine.get_u_prev(), u_in)), float(u0[0, 0]), float(u_in[0, 0, 0]))
         dist.barrier()
         q.put((rank, se.mode, res))
@@ -252,7 +252,8 @@ def _timeout_rank(rank, world, port, q):
 
 def test_peer_timeout_keeps_warm_start():
     """A rank whose peer never steps: its finalize blocks wait out the 2 s bound, then the step
-    keeps the warm start (u_prev unchanged, outputs from it, finite) and reports nonfinite = 2."""
+    keeps the warm start (u_prev unchanged, outputs from it, finite) and reports nonfinite = 2
+    (StepStats.nonfinite and .exchange_timeout)."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -271,7 +272,7 @@ def test_peer_timeout_keeps_warm_start():
                 p.kill()
     assert [r[1] for r in res] == ["peer", "peer"]
     dt, nonfinite, finite, kept, u0, u_in0 = res[0][2]
-    assert nonfinite == 2 and finite and kept, res[0][2]
+    assert nonfinite == (True, True) and finite and kept, res[0][2]
     assert u0 == u_in0, "u0 is the kept warm start's first step"
     assert 1.5 < dt < 30.0, dt
 
