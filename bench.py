@@ -445,7 +445,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                    "horizon": H, "action_dim": r["A"], "vehicles_per_gpu": V,
                    "noise": "device Philox4x32-10 (+2x32)", "state_dtype": "f64" if r["state_f64"] else "f32",
                    "parallelism": ((f"samples sharded over {world} GPUs, " +
-                                    ("peer exchange in the finalize/step" if r["exchange"] == "peer"
+                                    ("peer exchange inside each step's finalize" if r["exchange"] == "peer"
                                      else "1 all-reduce/step")) if world > 1 else "1 GPU")},
         "timing": {"timed_batches": len(r["batches_s"]), "steps_per_batch": args.steps,
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
