@@ -305,10 +305,15 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     red_dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else "cpu"
 
     def barrier():
+        # torch's synchronize first: it covers torch's own streams (idle here: the steps run on
+        # the engine's native queue or stream) and costs ~3 us of host time even on an idle
+        # device, which it now spends while the batch still runs; eng.synchronize() then waits
+        # for the batch's completion signal.  Both still bracket every batch.
+        torch.cuda.synchronize()
         eng.synchronize()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
 
     se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
     barrier()

@@ -147,9 +147,13 @@ def probe_batch():
         engines[m].run_steps(50)
         engines[m].synchronize()
     ns = [1, 2, 5, 10, 20, 50, 200]
-    res = {m: {} for m in engines}
+    # "aql_t": the same native engine with torch's synchronize ahead of the engine's (bench.py's
+    # bracket since round 4: torch's idle-device cost overlaps the running batch)
+    variants = [("hip", "hip", False), ("aql", "aql", False), ("aql_t", "aql", True)]
+    res = {m: {} for m, _, _ in variants}
     for _ in range(15):
-        for m, e in engines.items():
+        for m, em, torch_first in variants:
+            e = engines[em]
             for n in ns:
                 e.run_steps(10)   # priming, untimed
                 e.synchronize()
@@ -157,9 +161,14 @@ def probe_batch():
                 t0 = time.perf_counter()
                 e.run_steps(n)
                 t1 = time.perf_counter()
-                e.synchronize()
-                ts = time.perf_counter()
-                torch.cuda.synchronize()
+                if torch_first:
+                    torch.cuda.synchronize()
+                    ts = time.perf_counter()
+                    e.synchronize()
+                else:
+                    e.synchronize()
+                    ts = time.perf_counter()
+                    torch.cuda.synchronize()
                 t2 = time.perf_counter()
                 e.synchronize()          # both again, idle: the bracket's own host cost
                 ti = time.perf_counter()
@@ -167,7 +176,7 @@ def probe_batch():
                 tj = time.perf_counter()
                 res[m].setdefault(n, []).append(((t2 - t0) * 1e6, (t1 - t0) * 1e6, (ts - t1) * 1e6,
                                                  (t2 - ts) * 1e6, (ti - t2) * 1e6, (tj - ti) * 1e6))
-    for m in engines:
+    for m in res:
         tot = [np.median([x[0] for x in res[m][n]]) for n in ns]
         enq = [np.median([x[1] for x in res[m][n]]) for n in ns]
         slope, icpt = np.polyfit(ns, tot, 1)
@@ -175,7 +184,7 @@ def probe_batch():
               f"  | fit: {slope:.2f} us/step + {icpt:.1f} us per batch; n=20 -> {tot[ns.index(20)] / 20:.2f} us/step")
         for n in (1, 20):
             med = np.median(np.array(res[m][n]), axis=0)
-            print(f"  {m} n={n}: run_steps call {med[1]:.1f}, engine sync {med[2]:.1f}, torch sync {med[3]:.1f} us; "
+            print(f"  {m} n={n}: run_steps call {med[1]:.1f}, first sync {med[2]:.1f}, second sync {med[3]:.1f} us; "
                   f"idle: engine sync {med[4]:.1f}, torch sync {med[5]:.1f} us")
 
 
