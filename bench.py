@@ -9,13 +9,15 @@ state-steps, plus control-step p50 latency).
 A "step" is one MPPI control step (noise -> rollout -> FK -> cost -> softmin ->
 SavGol -> update) over one batch of synthetic state/goal input.
 
-Workloads:
-* plain ``python bench.py`` (N=1): ``arm_c3`` -- the configuration BASELINE.json's
-  metric is quoted on (Kinova arm, K=4096 H=32, configs[2]); ``scaling`` "weak".
-* under torch.distributed.run (WORLD_SIZE set, any N): ``c4`` -- the north star,
-  whole-body K=65536 H=64 (configs[3]) with the samples split 65536/N per rank (strong
-  scaling at the fixed K), one RCCL all-reduce per step; ``scaling`` "strong".  The N=1
-  line of that curve is also in every plain N=1 run as ``secondary.c4``.
+Workloads (the same primary workload at every N, so the driver's per-N values form one curve):
+* ``arm_c3`` -- the configuration BASELINE.json's metric is quoted on (Kinova arm, K=4096
+  H=32, configs[2]).  At N=1 it is the plain control step.  Under torch.distributed.run
+  (N ranks) every rank runs the K=4096 H=32 step as its shard of one K=4096*N controller
+  (global samples [g*4096, (g+1)*4096), the ranks' softmin partials combined every step by
+  the peer exchange): per-GPU work fixed, ``scaling`` "weak".
+* ``secondary.c4`` -- the north star, whole-body K=65536 H=64 (configs[3]) with the samples
+  split 65536/N per rank (strong scaling at the fixed K), at every N: in the plain N=1 run
+  (one GPU, K=65536) and in every N>1 run (``--secondary-multi``).
 ``value`` is the whole job's rollout-steps per second with state and warm start resident
 on the GPU (back-to-back steps, one host sync), bracketed by barrier + synchronize on
 both sides and the max over ranks.  The host-inclusive call latency (state H2D, outputs,
@@ -488,9 +490,12 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
 
 def secondary_entry(s, ns):
     rf = roofline_of(s, ns)
-    e = {"value": s["V"] * s["K"] * s["H"] / (s["dt"] / ns), "ms_per_step": 1e3 * s["dt"] / ns,
+    e = {"value": s["world"] * s["V"] * s["K"] * s["H"] / (s["dt"] / ns), "unit": "rollout-steps/s",
+         "ms_per_step": 1e3 * s["dt"] / ns,
          "latency_p50_ms": float(np.median(np.array(s["lat"]) * 1e3)) if s["lat"] else None,
-         "samples": s["K"], "horizon": s["H"], "vehicles": s["V"],
+         "n_gpus": s["world"], "scaling": "strong" if s["strong"] else "weak",
+         "samples": s["K"], "samples_total": s["world"] * s["K"],
+         "horizon": s["H"], "vehicles": s["V"],
          "rollout_kernel_us": rf["kernel_us"], "rollout_back_to_back_us": s["tim"]["rollout_us"],
          "finalize_us": s["tim"]["finalize_us"], "rollout_GBps": rf["achieved"],
          "roofline_frac": rf["frac"], "roofline_frac_back_to_back": rf["frac_back_to_back"],
@@ -498,6 +503,9 @@ def secondary_entry(s, ns):
     if s["native"]:
         e.update({"exchange": s.get("exchange", "rccl"), "allreduce_us": s["tim"].get("allreduce_us"),
                   "rccl_nranks": s["rccl_nranks"]})
+    if s["world"] > 1:
+        e.update({"exchange": s["exchange"], "native_comm_error": s["native_error"],
+                  "rollout_us_max_over_ranks": s["tim"].get("rollout_in_step_us_max_over_ranks")})
     return e
 
 
@@ -546,7 +554,9 @@ def main():
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="leave the process's CPU affinity alone (default: bind to the GPU's local CPUs)")
     ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4_shard_peer1,c4,fleet_c5,quadrotor_c2",
-                    help="extra workloads reported (N=1 only), comma separated; '' for none")
+                    help="extra workloads reported at N=1, comma separated; '' for none")
+    ap.add_argument("--secondary-multi", default="c4",
+                    help="extra workloads reported at N>1 (every rank runs them), comma separated; '' for none")
     args = ap.parse_args()
     # the JSON line is the only thing on stdout: keep the real stdout for it and send fd 1 to
     # stderr, so native libraries that print there (RCCL's version banner at communicator
@@ -559,7 +569,9 @@ def main():
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    workload = args.workload or ("c4" if launched else "arm_c3")
+    # one primary workload at every N (arm_c3: the metric's configuration; weak-scaled under
+    # torchrun), so the N=1 point of a scaling curve measures what the N>1 points do
+    workload = args.workload or "arm_c3"
     # ranks beyond the visible devices wrap (rehearsing N ranks on fewer GPUs)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     # the launching thread on the GPU's own socket (quadrotor_manipulator_mppi_amd.affinity);
@@ -590,10 +602,11 @@ def main():
     r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
                      timing=not args.no_kernel_timing, batches=batches)
     secondary = {}
-    if world == 1 and args.secondary and r["tim"] is not None:
-        for wname in [s for s in args.secondary.split(",") if s and s != workload]:
+    extra = args.secondary if world == 1 else args.secondary_multi
+    if extra and r["tim"] is not None:
+        for wname in [s for s in extra.split(",") if s and s != workload]:
             ns = max(50, args.steps // 5)
-            s = run_workload(wname, ns, 20, 1, None, 50, batches=3)
+            s = run_workload(wname, ns, 20, world, dist, 50, batches=3)   # (every rank, in lockstep)
             secondary[wname] = secondary_entry(s, ns)
             log(f"secondary {wname}: {secondary[wname]}")
     dropin = None

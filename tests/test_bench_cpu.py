@@ -106,3 +106,27 @@ def test_bench_line_native_one_rank_and_traffic_by_shape():
 
 def test_auto_batches():
     assert bench.auto_batches(20) == 7 and bench.auto_batches(500) == 3 and bench.auto_batches(5000) == 1
+
+
+def test_primary_weak_and_c4_secondary_at_two_ranks():
+    """Under torchrun the primary stays the metric's arm_c3 shape, weak-scaled (K=4096 per
+    rank, total 4096*N), so a scaling curve's N=1 point measures what its N>1 points do; the
+    north-star c4 (K=65536 split over the ranks) is reported beside it as secondary.c4 with
+    the whole job's rollout-steps/s."""
+    r = _fake_result(2, 0, model="arm", K=4096, H=32)
+    r.update(A=7, strong=False, bytes=4096 * 32 * 76 + 4 * 4096, state_f64=True, exchange="peer", native=True,
+             rccl_nranks=None, rccl_rank=None)
+    r["dt"] = float(np.median(r["batches_s"]))
+    line = bench.make_line("arm_c3", r, _args())
+    step = r["dt"] / 20
+    assert line["scaling"] == "weak" and line["n_gpus"] == 2
+    assert line["config"]["samples_per_gpu"] == 4096 and line["config"]["samples_total"] == 8192
+    assert line["value"] == pytest.approx(2 * 4096 * 32 / step)
+    assert "peer exchange" in line["config"]["parallelism"] and line["multi_gpu"]["exchange"] == "peer"
+    s = _fake_result(2, 0, K=32768)
+    s["dt"] = float(np.median(s["batches_s"]))
+    s["tim"]["rollout_in_step_us_max_over_ranks"] = 13.6
+    e = bench.secondary_entry(s, 20)
+    assert e["n_gpus"] == 2 and e["scaling"] == "strong" and e["samples_total"] == 65536
+    assert e["value"] == pytest.approx(65536 * 64 / (s["dt"] / 20))
+    assert e["rollout_us_max_over_ranks"] == 13.6 and e["exchange"] == "torch"
