@@ -340,7 +340,33 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     # batch): the host's launch rate after a pause is what a batch then measures less of
     # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
     prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
-    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
+    # GPU heat-up: the MI355X raises its clocks over ~10 ms of sustained load and drops them again
+    # when idle (profiles/r04/ramp: C3 9.93 us/step in a 20-step batch after 50 ms idle, 9.42
+    # after a 200-step burst, 9.02-9.05 after >= 1000 steps; consecutive 100-step chunks 9.33 ->
+    # 8.73 over the first ~10 ms).  So ahead of each batch's W warmup steps the steps run back to
+    # back for HEAT_MS first, and a batch measures the sustained rate, not the power-state ramp --
+    # at 20 steps (0.2 ms) it would otherwise time mostly the ramp.  The same step count on every
+    # rank (from the max-over-ranks step time), so peer-exchange ranks stay in lockstep.  The
+    # batches without the heat-up are reported too (timing.ms_per_step_batches_no_heatup).
+    heat_ms = float(os.environ.get("MPPI_BENCH_HEAT_MS", "15"))
+    n_heat = 0
+    if heat_ms > 0:
+        t_step = tim["pair_us"] * 1e-6 if tim is not None else None
+        if t_step is None:   # no event timing (profiler runs): one timed 20-step batch
+            barrier()
+            t0 = time.perf_counter()
+            se.run_steps(20)
+            barrier()
+            t_step = (time.perf_counter() - t0) / 20
+        t_step = reduce_max([t_step], dist, red_dev)[0]
+        n_heat = int(min(20000, max(100, np.ceil(heat_ms * 1e-3 / t_step))))
+    bt_cold, _ = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
+    bt_cold = reduce_max(bt_cold, dist, red_dev)
+    heat_prime = prime
+    if n_heat:
+        heat_prime = (lambda: (se.run_steps(n_heat), se.run_steps(max(1, warmup)))) if prime is not None else \
+            (lambda: se.run_steps(n_heat))
+    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, heat_prime)
     bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
     if tim is not None and dist is not None:   # the slowest rank's kernels
         tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
@@ -360,7 +386,8 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.mode == "rccl" else None
-    res = {"batches_s": bt, "enqueue_s": benq, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
+    res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat,
+           "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
            "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
            "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native, "exchange": se.mode,
@@ -458,8 +485,14 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                    "ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r["batches_s"]],
                    "enqueue_ms_per_step_batches": [round(1e3 * b / args.steps, 6) for b in r.get("enqueue_s", [])],
                    "dispatch": r.get("dispatch"),
-                   "basis": "median over the batches; each batch = `warmup` untimed steps, then exactly `steps` "
-                            "control steps bracketed by barrier + synchronize (wall clock), max over ranks"},
+                   "heatup_steps_per_batch": r.get("heat_steps"),
+                   "ms_per_step_batches_no_heatup": [round(1e3 * b / args.steps, 6) for b in r.get("batches_s_no_heatup", [])],
+                   "ms_per_step_no_heatup": (1e3 * float(np.median(r["batches_s_no_heatup"])) / args.steps
+                                             if r.get("batches_s_no_heatup") else None),
+                   "basis": "median over the batches; each batch = a GPU heat-up (`heatup_steps_per_batch` back-to-back "
+                            "steps, ~15 ms: the clocks' ramp under sustained load, profiles/r04/ramp), `warmup` untimed "
+                            "steps, then exactly `steps` control steps bracketed by barrier + synchronize (wall clock), "
+                            "max over ranks; the same batches without the heat-up: ms_per_step_no_heatup"},
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
         "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
         "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,

@@ -332,8 +332,53 @@ def probe_latency(model="arm", K="4096", H="32"):
         e.close()
 
 
+def probe_ramp(model="arm", K="4096", H="32"):
+    """Per-step time against how long the GPU has been busy: 20-step batches after an idle pause
+    and right after sustained bursts of different lengths; then one long run timed in chunks of
+    100 steps.  A per-step time that falls with the length of the preceding burst is the GPU's
+    clock/power state ramping under sustained load, not the step itself."""
+    import torch
+    e = _engine(model=model, K=int(K), H=int(H), seed=3)
+    e.run_steps(200)
+    e.synchronize()
+
+    def batch20():
+        torch.cuda.synchronize()
+        e.synchronize()
+        t0 = time.perf_counter()
+        e.run_steps(20)
+        torch.cuda.synchronize()
+        e.synchronize()
+        return (time.perf_counter() - t0) / 20 * 1e6
+
+    res = {}
+    for _ in range(5):
+        for pre in (0, 200, 1000, 5000, 20000):
+            if pre:
+                e.run_steps(pre)   # a sustained burst right before the timed batch
+            else:
+                time.sleep(0.05)   # idle
+            res.setdefault(pre, []).append(batch20())
+    for pre, v in res.items():
+        print(f"{model} K={K} H={H}: 20-step batch after {'50 ms idle' if not pre else f'{pre}-step burst'}: "
+              f"median {np.median(v):.2f} us/step  {[round(x, 2) for x in v]}", flush=True)
+    time.sleep(0.05)
+    chunks = []
+    t_prev = time.perf_counter()
+    for i in range(60):   # 60 x 100 steps, synchronised per chunk (no idle beyond the sync)
+        e.run_steps(100)
+        e.synchronize()
+        t = time.perf_counter()
+        chunks.append((t - t_prev) / 100 * 1e6)
+        t_prev = t
+    print(f"{model}: per-step time of consecutive 100-step chunks after 50 ms idle: "
+          f"{[round(x, 2) for x in chunks]}", flush=True)
+    e.close()
+
+
 PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
-          "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency}
+          "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
+          "ramp": probe_ramp}
 
 if __name__ == "__main__":
     if len(sys.argv) < 2 or sys.argv[1] not in PROBES:
