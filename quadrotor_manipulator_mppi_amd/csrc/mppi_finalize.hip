@@ -317,30 +317,44 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             nv[r] = (r == xme) ? N : 0.0f;
             hv[r] = (r == xme) ? hown : 0.0f;
         }
+        // Poll: every pending rank's words are loaded in ONE batch per round (each lane its column
+        // word and, lanes < 4, a header word; global, not flat, loads into separate registers), then
+        // checked together, so a round costs one memory round trip whatever the rank count.  (With
+        // the loads issued per rank behind divergent branches, the compiler waited for each load
+        // before the next: 2 (G - 1) serial round trips per round, ~14 at G = 8.)  Which ranks are
+        // still pending is wave-uniform: a rank is done when every lane that needs a word of it has
+        // seen the step's tag (a ballot), and its words are taken from that round.
+        typedef __attribute__((address_space(1))) unsigned long long gu64;
         const bool needc = lane < W, needh = lane < kHdr;
-        uint32_t pend = (needc || needh) ? ((1u << xn) - 1u) & ~(1u << xme) : 0u;
+        uint32_t pend = ((1u << xn) - 1u) & ~(1u << xme);   // (uniform)
         const unsigned long long* src = xlocal + (par * (size_t)xn * nbk + blk) * kXW;
         const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
         bool late = false;
-        while (__builtin_amdgcn_ballot_w64(pend != 0u) != 0ull) {
+        while (pend != 0u) {
+            unsigned long long xc[kMaxPeers], xh[kMaxPeers];
+#pragma unroll
+            for (int r = 0; r < kMaxPeers; ++r) {
+                xc[r] = 0ull; xh[r] = 0ull;
+                if ((pend >> r) & 1u) {   // (uniform branch)
+                    gu64* s = (gu64*)(src + (size_t)r * nbk * kXW);
+                    // lane < 64 <= kXW - kHdr: every lane's word lies inside the rank's slot (the
+                    // words past W are not written and not checked)
+                    xc[r] = __hip_atomic_load(s + kHdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    xh[r] = __hip_atomic_load(s + (lane & (kHdr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < kMaxPeers; ++r) {
                 if (!((pend >> r) & 1u)) continue;
-                const unsigned long long* s = src + (size_t)r * nbk * kXW;
-                bool ok = true;
-                if (needc) {
-                    const unsigned long long x = __hip_atomic_load(s + kHdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    ok = (uint32_t)(x >> 32) == tag;
-                    nv[r] = __uint_as_float((uint32_t)x);
+                const bool ok = (!needc || (uint32_t)(xc[r] >> 32) == tag) && (!needh || (uint32_t)(xh[r] >> 32) == tag);
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {
+                    nv[r] = needc ? __uint_as_float((uint32_t)xc[r]) : 0.0f;
+                    hv[r] = needh ? __uint_as_float((uint32_t)xh[r]) : 0.0f;
+                    pend &= ~(1u << r);
                 }
-                if (needh) {
-                    const unsigned long long y = __hip_atomic_load(s + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    ok = ok && (uint32_t)(y >> 32) == tag;
-                    hv[r] = __uint_as_float((uint32_t)y);
-                }
-                if (ok) pend &= ~(1u << r);
             }
-            if (__builtin_amdgcn_ballot_w64(pend != 0u) == 0ull) break;
+            pend = __builtin_amdgcn_readfirstlane(pend);
+            if (pend == 0u) break;
             if (__builtin_amdgcn_s_memrealtime() - t_in > kPeerWaitTicks) { late = true; break; }   // (2 s)
             __builtin_amdgcn_s_sleep(1);
         }
