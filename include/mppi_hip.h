@@ -267,6 +267,13 @@ mppi_status mppi_exchange(mppi_engine* e);
  * Not combinable with mppi_comm_init / mppi_bind_exchange on the same engine. */
 mppi_status mppi_peer_open(mppi_engine* e, uint8_t handle[MPPI_PEER_HANDLE_BYTES]);
 mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles /* shard_count x MPPI_PEER_HANDLE_BYTES */);
+/* The same connection for ranks inside ONE process (one process driving several engines: on one
+ * GPU, or on several GPUs with peer access): mppi_peer_region returns this engine's region as a
+ * device address after mppi_peer_open, and mppi_peer_connect_ptrs takes every rank's address in
+ * rank order (this engine's own included) instead of IPC handles.  Every engine's steps must then
+ * be in flight together (native dispatch: mppi_run_steps returns once the packets are queued). */
+mppi_status mppi_peer_region(mppi_engine* e, uint64_t* device_address);
+mppi_status mppi_peer_connect_ptrs(mppi_engine* e, const uint64_t* device_addresses /* shard_count */);
 /* Connection check (collective, before the first step; a barrier between phases): phase 0 copies
  * a pattern word into this rank's slot of every rank's region; phase 1 checks that this rank's
  * region holds every rank's word (MPPI_OK, else MPPI_ERR_COMM) and clears it; phase 2 runs the

@@ -103,6 +103,8 @@ PROTOTYPES = {
     "mppi_peer_open": (_ST, [_P, C.POINTER(C.c_uint8)]),
     "mppi_peer_connect": (_ST, [_P, C.POINTER(C.c_uint8)]),
     "mppi_peer_probe": (_ST, [_P, C.c_int32]),
+    "mppi_peer_region": (_ST, [_P, C.POINTER(C.c_uint64)]),
+    "mppi_peer_connect_ptrs": (_ST, [_P, C.POINTER(C.c_uint64)]),
     "mppi_comm_info": (_ST, [_P, _I32, _I32]),
     "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),

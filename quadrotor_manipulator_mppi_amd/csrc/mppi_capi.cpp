@@ -1307,6 +1307,23 @@ mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
     return MPPI_OK;
 }
 
+// the regions' device addresses, in rank order, into the finalize's tail (both connects)
+static mppi_status peer_bind(mppi_engine* e, const std::vector<unsigned long long*>& ptrs) {
+    const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
+    if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
+    HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
+    FinParams& f = e->fp;
+    f.xpeers = e->d_xpeers; f.xlocal = e->d_xregion; f.xn = n; f.xme = me;
+    FinTail t[2] = {tail_of(f, 0), tail_of(f, 2)};
+    t[0].wraw = t[0].wsmooth = nullptr;   // (as at create: the step's FINAL stores no readback copies)
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(e->d_tail + kTailFinal, &t[0], sizeof(FinTail), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_tail + kTailReadback, &t[1], sizeof(FinTail), hipMemcpyHostToDevice));
+    e->peer = true;
+    e->call_cached = false;
+    return MPPI_OK;
+}
+
 mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles) {
     if (!e || !handles) return fail(MPPI_ERR_INVALID_ARG, "null argument");
     if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_connect before mppi_peer_open");
@@ -1328,18 +1345,30 @@ mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles) {
         e->x_opened[r] = q;
         ptrs[r] = (unsigned long long*)q;
     }
-    if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
-    HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
-    FinParams& f = e->fp;
-    f.xpeers = e->d_xpeers; f.xlocal = e->d_xregion; f.xn = n; f.xme = me;
-    FinTail t[2] = {tail_of(f, 0), tail_of(f, 2)};
-    t[0].wraw = t[0].wsmooth = nullptr;   // (as at create: the step's FINAL stores no readback copies)
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    HIP_TRY(hipMemcpy(e->d_tail + kTailFinal, &t[0], sizeof(FinTail), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_tail + kTailReadback, &t[1], sizeof(FinTail), hipMemcpyHostToDevice));
-    e->peer = true;
-    e->call_cached = false;
+    return peer_bind(e, ptrs);
+}
+
+mppi_status mppi_peer_region(mppi_engine* e, uint64_t* device_address) {
+    if (!e || !device_address) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_region before mppi_peer_open");
+    *device_address = (uint64_t)(uintptr_t)e->d_xregion;
     return MPPI_OK;
+}
+
+mppi_status mppi_peer_connect_ptrs(mppi_engine* e, const uint64_t* device_addresses) {
+    if (!e || !device_addresses) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_connect_ptrs before mppi_peer_open");
+    if (e->peer) return fail(MPPI_ERR_STATE, "peer exchange already connected");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
+    if (device_addresses[me] != (uint64_t)(uintptr_t)e->d_xregion)
+        return fail(MPPI_ERR_INVALID_ARG, "mppi_peer_connect_ptrs: entry %d is not this engine's region", me);
+    std::vector<unsigned long long*> ptrs(n, nullptr);
+    for (int r = 0; r < n; ++r) {
+        if (!device_addresses[r]) return fail(MPPI_ERR_INVALID_ARG, "mppi_peer_connect_ptrs: null region of rank %d", r);
+        ptrs[r] = (unsigned long long*)(uintptr_t)device_addresses[r];
+    }
+    return peer_bind(e, ptrs);
 }
 
 // Connection check before the first step (distributed.py), three phases with a barrier between

@@ -227,6 +227,17 @@ class Engine:
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         capi.check(self._L.mppi_peer_connect(self._h, buf), "peer_connect")
 
+    def peer_region(self) -> int:
+        """This engine's exchange region as a device address (after peer_open; mppi_peer_region)."""
+        x = C.c_uint64(0)
+        capi.check(self._L.mppi_peer_region(self._h, C.byref(x)), "peer_region")
+        return int(x.value)
+
+    def peer_connect_ptrs(self, addresses):
+        """In-process ranks: every rank's region address in rank order (mppi_peer_connect_ptrs)."""
+        buf = (C.c_uint64 * len(addresses))(*[int(a) for a in addresses])
+        capi.check(self._L.mppi_peer_connect_ptrs(self._h, buf), "peer_connect_ptrs")
+
     def peer_probe(self, phase: int):
         """Connection check (collective): phase 0 on every rank, a barrier, then phase 1."""
         capi.check(self._L.mppi_peer_probe(self._h, int(phase)), "peer_probe")

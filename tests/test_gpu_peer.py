@@ -10,10 +10,12 @@ every rank's exchange region as tagged 8 B words and combines the ranks' partial
     engine over all 8192 samples, both ranks finalise bit-identically, and u0 / u_prev / outputs
     equal the one-engine step at the north star's rtol 1e-4 (the ranks' partials are combined in
     another order than the blocks' records);
-(c) a probe word that never arrives fails the connection on every rank.
-More ranks than two do not fit one GPU this way: every finalize block of every rank waits for
-the same block of the others, and one CU holds one finalize block, so 8 ranks' blocks would
-need more CUs than the GPU has (on a node each rank has its own GPU).
+(c) a probe word that never arrives fails the connection on every rank;
+(d) 4 and 8 ranks as engines of ONE process on this GPU (mppi_peer_connect_ptrs: the regions'
+    device addresses instead of IPC handles), each with its own native queue, every engine's
+    batch in flight together: the rank counts of a node's scaling run on one GPU.
+More than two ranks as separate processes are not run on one GPU (the box's process limits and
+queue oversubscription; on a node each rank has its own GPU).
 """
 import os
 import socket
@@ -285,3 +287,64 @@ def test_peer_probe_failure_falls_back_on_every_rank():
     modes = {r[1] for r in res}
     assert len(modes) == 1 and "peer" not in modes, modes
     assert all("peer exchange" in (r[2] or "") for r in res), [r[2] for r in res]
+
+
+@pytest.mark.parametrize("G", [4, 8])
+def test_peer_in_process_ranks_equal_one_engine(G):
+    """(d) G ranks as G engines in ONE process on this GPU (mppi_peer_region /
+    mppi_peer_connect_ptrs): the rank counts of a node's scaling run, which separate processes
+    cannot host on one GPU, with every engine's native batch in flight together.  Whole-body
+    K = G x 512, H = 64, against one engine over all G x 512 samples: per-global-k costs
+    bit-identical, every rank finalises bit-identically, u_prev at rtol 1e-4; then a 40-step batch
+    on every engine, still bit-identical across ranks, and no exchange timeout."""
+    k = 512
+    full = _engine(n_samples=G * k)
+    full.set_state(STATE)
+    steps = []
+    for s in range(2):
+        u_in = full.get_u_prev()[0]
+        full.run_steps(1)
+        full.synchronize()
+        steps.append(dict(u_in=u_in, S=full.get_costs()[0], u_out=full.get_u_prev()[0]))
+    full.close()
+    ranks = [_engine(n_samples=k, shard_rank=r, shard_count=G) for r in range(G)]
+    try:
+        for e in ranks:
+            e.peer_open()
+        addrs = [e.peer_region() for e in ranks]
+        for e in ranks:
+            e.peer_connect_ptrs(addrs)
+            e.set_state(STATE)
+        for s in range(2):
+            for e in ranks:
+                e.set_u_prev(steps[s]["u_in"])
+            for e in ranks:   # queued on every engine's native queue, then waited for
+                e.run_steps(1)
+            for e in ranks:
+                e.synchronize()
+            S = np.concatenate([e.get_costs()[0] for e in ranks])
+            assert np.array_equal(S, steps[s]["S"]), f"step {s}: per-global-k costs"
+            ups = [e.get_u_prev()[0] for e in ranks]
+            for r in range(1, G):
+                assert np.array_equal(ups[r], ups[0]), f"step {s}: rank {r} finalised differently"
+            _close(ups[0], steps[s]["u_out"], rtol=1e-4, atol=1e-6, what=f"step {s}: u_prev")
+        for e in ranks:
+            e.run_steps(40)
+        for e in ranks:
+            e.synchronize()
+        ups = [e.get_u_prev()[0] for e in ranks]
+        assert all(np.array_equal(u, ups[0]) for u in ups) and np.isfinite(ups[0]).all()
+        for e in ranks:
+            out, u0, st = e.read_outputs()
+            assert not st[0].nonfinite and not st[0].exchange_timeout
+        assert all(e.dispatch_info().startswith("aql;") for e in ranks), [e.dispatch_info() for e in ranks]
+        with pytest.raises(Exception):   # another engine's address in this engine's own slot
+            bad = _engine(n_samples=k, shard_rank=0, shard_count=2)
+            bad.peer_open()
+            try:
+                bad.peer_connect_ptrs([addrs[1], addrs[0]])
+            finally:
+                bad.close()
+    finally:
+        for e in ranks:
+            e.close()
