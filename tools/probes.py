@@ -376,9 +376,47 @@ def probe_ramp(model="arm", K="4096", H="32"):
     e.close()
 
 
+def probe_peer_ranks(model="arm", K="512", H="32", Gs="1,2,4,8"):
+    """Per-step time of G peer-exchange ranks as engines of this one process (mppi_peer_connect_ptrs),
+    every engine's 200-step native batch in flight together, K samples per engine: with small K the
+    rollouts hardly contend and the G-rank step over the 1-engine step is the exchange's cost on
+    one GPU (G = 1: a plain engine).  Median of 7 batches after a 15 ms heat-up per batch."""
+    import torch
+    for G in [int(g) for g in Gs.split(",")]:
+        es = [_engine(model=model, K=int(K), H=int(H), seed=3, shard_rank=r, shard_count=G) for r in range(G)]
+        if G > 1:
+            for e in es:
+                e.peer_open()
+            addrs = [e.peer_region() for e in es]
+            for e in es:
+                e.peer_connect_ptrs(addrs)
+        for e in es:
+            e.run_steps(200)
+        for e in es:
+            e.synchronize()
+        ts = []
+        for _ in range(7):
+            for e in es:
+                e.run_steps(2000)   # heat-up
+            for e in es:
+                e.synchronize()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for e in es:
+                e.run_steps(200)
+            for e in es:
+                e.synchronize()
+            ts.append((time.perf_counter() - t0) / 200 * 1e6)
+        bad = sum(bool(e.read_outputs()[2][0].nonfinite) for e in es)
+        print(f"{model} K={K}/engine H={H} G={G}: {np.median(ts):.2f} us/step (batches {[round(x, 2) for x in ts]})"
+              f"{'  NONFINITE/TIMEOUT on %d engines' % bad if bad else ''}", flush=True)
+        for e in es:
+            e.close()
+
+
 PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
-          "ramp": probe_ramp}
+          "ramp": probe_ramp, "peer_ranks": probe_peer_ranks}
 
 if __name__ == "__main__":
     if len(sys.argv) < 2 or sys.argv[1] not in PROBES:
