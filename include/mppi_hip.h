@@ -270,8 +270,9 @@ mppi_status mppi_peer_connect(mppi_engine* e, const uint8_t* handles /* shard_co
 /* The same connection for ranks inside ONE process (one process driving several engines: on one
  * GPU, or on several GPUs with peer access): mppi_peer_region returns this engine's region as a
  * device address after mppi_peer_open, and mppi_peer_connect_ptrs takes every rank's address in
- * rank order (this engine's own included) instead of IPC handles.  Every engine's steps must then
- * be in flight together (native dispatch: mppi_run_steps returns once the packets are queued). */
+ * rank order (this engine's own included) instead of IPC handles; across GPUs the caller enables
+ * peer access first (hipDeviceEnablePeerAccess).  Every engine's steps must then be in flight
+ * together (native dispatch: mppi_run_steps returns once the packets are queued). */
 mppi_status mppi_peer_region(mppi_engine* e, uint64_t* device_address);
 mppi_status mppi_peer_connect_ptrs(mppi_engine* e, const uint64_t* device_addresses /* shard_count */);
 /* Connection check (collective, before the first step; a barrier between phases): phase 0 copies
