@@ -147,6 +147,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     uint32_t* flags = nullptr;
     const VehicleConst* vcb = nullptr;
     unsigned long long* const* xpeers = nullptr;   // peer exchange (null: off)
+    unsigned long long xpl = 0ull;   // lane d < xn: rank d's region address (wave 0's stores read it by readlane)
     unsigned long long* xlocal = nullptr;
     int32_t xn = 0, xme = 0;
     uint32_t xstep = 0u;
@@ -184,6 +185,12 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             if (seq == kSeqFromVc) seqv = ld_dev((const uint32_t*)vcp->_pad);   // (its bits)
         }
         if (tid == 0 && xpeers) xstep = ld_dev((const uint32_t*)(vcb + v) + kVcStepWord);   // the exchange's tag
+        // every rank's region address, one per lane, loaded here so it lands during the record fold:
+        // loaded per rank inside the store loop, each pointer load's wait also waited for the
+        // previous rank's system-scope stores to complete (vmcnt counts stores): G - 1 serial
+        // remote-store completions before the poll could even start
+        if (wv == 0 && xpeers)
+            xpl = ((const __attribute__((address_space(1))) unsigned long long*)xpeers)[lane < xn ? lane : 0];
     };
     // running softmin per lane.  The header terms (rho, eta, eta2, nan) are the same for every
     // column of a row group, so each lane carries them and the wave fold runs over row groups
@@ -304,9 +311,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
             const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
             const size_t off = ((par * (size_t)xn + (size_t)xme) * nbk + blk) * kXW;
-            for (int d = 0; d < xn; ++d) {
-                if (d == xme) continue;
-                unsigned long long* dst = uniform_ptr(xpeers[d]) + off;
+            typedef __attribute__((address_space(1))) unsigned long long gst64;
+#pragma unroll
+            for (int d = 0; d < kMaxPeers; ++d) {   // (uniform branches; no wait between the ranks' stores)
+                if (d >= xn || d == xme) continue;
+                const uint64_t pa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(xpl >> 32), d) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)xpl, d);
+                gst64* dst = (gst64*)pa + off;
                 if (lane < W) __hip_atomic_store(dst + kHdr + lane, wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (lane < kHdr) __hip_atomic_store(dst + lane, wh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
