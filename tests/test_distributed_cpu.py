@@ -197,6 +197,9 @@ def test_native_comm_entry_points_reject_bad_arguments():
     assert L.mppi_peer_open(None, h) == capi.ERR_INVALID_ARG
     assert L.mppi_peer_connect(None, h) == capi.ERR_INVALID_ARG
     assert L.mppi_peer_probe(None, 0) == capi.ERR_INVALID_ARG
+    addr = (C.c_uint64 * 8)()
+    assert L.mppi_peer_region(None, addr) == capi.ERR_INVALID_ARG
+    assert L.mppi_peer_connect_ptrs(None, addr) == capi.ERR_INVALID_ARG
     assert "null" in L.mppi_last_error().decode()
 
 
