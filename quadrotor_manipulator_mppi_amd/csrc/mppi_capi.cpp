@@ -246,9 +246,20 @@ void mul34(const float* A, const float* B, float* C) {
     std::memcpy(C, r, sizeof(r));
 }
 
+// The joints' constant parts for the host FK: origin transforms (rpy -> R: six libm trig calls per
+// joint) and unit axes.  An engine computes them once (mppi_create); per control call they were
+// ~1.5 us of check_reach's ~2 us.
+void fk_consts(const mppi_joint* joints, int nj, float* O16s, float* axes) {
+    for (int n = 0; n < nj; ++n) {
+        joint_origin(joints[n], O16s + 16 * n);
+        unit_axis(joints[n], axes + 3 * n);
+    }
+}
+
 // Host FK at one joint vector (check_reach path, urdf_fk.py:60-75 +
 // urdfparser.py:166-206): cos/sin in the state dtype, transforms in fp32.
-void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xyzquat, bool f64, float* out16) {
+void host_fk_c(const mppi_joint* joints, int nj, const float* O16s, const float* axes, const double* q,
+               const double* xyzquat, bool f64, float* out16) {
     float T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     auto mul = [](const float* A, const float* B, float* C) {
         float r[16];
@@ -262,11 +273,10 @@ void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xy
     };
     for (int n = 0; n < nj; ++n) {
         const mppi_joint& j = joints[n];
-        float O[16], L[16];
-        joint_origin(j, O);
+        const float* O = O16s + 16 * n;
+        const float* a = axes + 3 * n;
+        float L[16];
         if (j.type == MPPI_JOINT_REVOLUTE && j.q_index >= 0) {
-            float a[3];
-            unit_axis(j, a);
             const double qv = f64 ? q[j.q_index] : (double)(float)q[j.q_index];
             float c, s;
             if (f64) { c = (float)std::cos(qv); s = (float)std::sin(qv); }
@@ -278,8 +288,6 @@ void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xy
                            0, 0, 0, 1};
             mul(O, R, L);
         } else if (j.type == MPPI_JOINT_PRISMATIC && j.q_index >= 0) {
-            float a[3];
-            unit_axis(j, a);
             const float qf = (float)q[j.q_index];
             float S[16] = {1, 0, 0, a[0] * qf, 0, 1, 0, a[1] * qf, 0, 0, 1, a[2] * qf, 0, 0, 0, 1};
             mul(O, S, L);
@@ -292,6 +300,12 @@ void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xy
     if (f64) base_from_xyzquat_t<double>(xyzquat, B);
     else base_from_xyzquat_t<float>(xyzquat, B);
     mul(B, T, out16);
+}
+
+void host_fk(const mppi_joint* joints, int nj, const double* q, const double* xyzquat, bool f64, float* out16) {
+    std::vector<float> O((size_t)16 * nj), ax((size_t)3 * nj);
+    fk_consts(joints, nj, O.data(), ax.data());
+    host_fk_c(joints, nj, O.data(), ax.data(), q, xyzquat, f64, out16);
 }
 
 }  // namespace
@@ -337,6 +351,7 @@ struct mppi_engine {
     LaunchDesc batch_roll{}, batch_fin{};
     std::vector<double> rec_out;        // a read step's outputs assembled from its tagged records
     std::vector<float> rec_u0, rec_stats;
+    std::vector<float> fk_O, fk_ax;     // the joints' origins and unit axes for check_reach's host FK
     uint32_t seq_ctr = 0;               // last completion-flag value handed out: monotonic and
                                         // independent of step_ctr (mppi_set_step_counter rewinds that)
     bool event_wait = false;            // MPPI_EVENT_WAIT=1: wait on ev_out instead of polling flags
@@ -789,6 +804,9 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     e->out_dim = mppi_output_dim(&c);
     e->C = (c.model == MPPI_MODEL_DRONE) ? 3 : (c.model == MPPI_MODEL_QUADROTOR) ? 6 : e->A + 12;
     e->tpos.assign((size_t)3 * e->V, 0.0f);
+    e->fk_O.assign((size_t)16 * std::max(0, (int)e->cfg.n_joints), 0.0f);
+    e->fk_ax.assign((size_t)3 * std::max(0, (int)e->cfg.n_joints), 0.0f);
+    fk_consts(e->cfg.joints, e->cfg.n_joints, e->fk_O.data(), e->fk_ax.data());
     e->tquat.assign((size_t)4 * e->V, 0.0f);
     for (int v = 0; v < e->V; ++v) e->tquat[4 * v + 3] = 1.0f;
     e->state.assign((size_t)e->state_dim * e->V, 0.0);
@@ -1656,7 +1674,8 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
             const double* s = e->state.data() + (size_t)v * e->state_dim;
             const double* qdes = o + (size_t)v * e->out_dim;
             float T16[16];
-            host_fk(e->cfg.joints, e->cfg.n_joints, qdes, s, e->cfg.state_f64 != 0, T16);
+            host_fk_c(e->cfg.joints, e->cfg.n_joints, e->fk_O.data(), e->fk_ax.data(), qdes, s, e->cfg.state_f64 != 0,
+                      T16);
             const float err = std::fabs(T16[3] - e->tpos[3 * v]) + std::fabs(T16[7] - e->tpos[3 * v + 1]) +
                               std::fabs(T16[11] - e->tpos[3 * v + 2]);
             reach = err < e->cfg.reach_tol;
