@@ -253,7 +253,6 @@ struct Step {
     uint32_t call_slot = 0;
     mppi::LaunchDesc fin_call{};          // what the call's finalize block holds
     Kern kc_r, kc_f;
-    std::string kc_rname, kc_fname;       // the symbols kc_r / kc_f were looked up for
     bool call_valid = false;
     bool call_unread = false;             // the last call's outputs not yet seen (step_call_read)
     mppi::LaunchDesc roll{}, fin{};       // what the device blocks hold (step word as uploaded)
@@ -385,16 +384,9 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
                 s->step_word, first, ffirst, strcmp(roll.symbol, s->roll.symbol), strcmp(fin.symbol, s->fin.symbol));
     }
     Kern kr, kf;
-    if (s->kc_rname == roll.symbol && s->kc_fname == fin.symbol) {   // the last call's kernels (no
-        kr = s->kc_r;                                                // string build, hash and lock per call)
-        kf = s->kc_f;
-    } else {
-        {
-            std::lock_guard<std::mutex> lk(g_mu);
-            if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
-        }
-        s->kc_rname = roll.symbol;
-        s->kc_fname = fin.symbol;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
     }
     if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
     if (step_off + 4 > roll.arg_bytes) { *err = "step counter outside the rollout's arguments"; return -2; }
@@ -569,16 +561,9 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto p0 = now();
     Kern kr, kf;
-    if (s->kc_rname == roll.symbol && s->kc_fname == fin.symbol) {   // the last call's kernels (no
-        kr = s->kc_r;                                                // string build, hash and lock per call)
-        kf = s->kc_f;
-    } else {
-        {
-            std::lock_guard<std::mutex> lk(g_mu);
-            if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
-        }
-        s->kc_rname = roll.symbol;
-        s->kc_fname = fin.symbol;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
     }
     if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
     if (step_off + 4 > roll.arg_bytes || seq_off + 4 > roll.arg_bytes) { *err = "call words outside the arguments"; return -2; }
