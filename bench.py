@@ -61,9 +61,14 @@ WORKLOADS = {
     # the 6-DoF rigid-body quadrotor (commented out in the reference), drone sizes
     "quadrotor_c2": dict(model="quadrotor", n_samples=4096, n_horizon=32,
                          desc="6-DoF quadrotor MPPI K=4096 H=32 (SURVEY §8f rank 3; configs[1] sizes)"),
-    # configs[4] per-GPU share: 64 vehicles x K=8192 over 8 GPUs -> 8 vehicles per GPU
-    "fleet_c5": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=8,
-                     desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
+    # configs[4]: the 64-vehicle fleet, K=8192 H=64 each, its vehicles split over the ranks (SURVEY §8e:
+    # "prefer vehicles across GPUs", no exchange; 8 per GPU at N=8, all 64 on one GPU at N=1)
+    "fleet_c5": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=64, mode="vehicles", strong=True,
+                     desc="64-vehicle whole-body fleet K=8192 H=64, vehicles split over the GPUs, no exchange "
+                          "(BASELINE configs[4])"),
+    # configs[4] per-GPU share at N=8: 8 vehicles x K=8192 H=64 on one GPU
+    "fleet_c5_share": dict(model="wholebody", n_samples=8192, n_horizon=64, n_vehicles=8,
+                           desc="64-vehicle whole-body fleet, 8 vehicles x K=8192 H=64 per GPU (configs[4] share)"),
     # the N=8 rank's whole step on one GPU: the C4 shard through the engine-owned RCCL
     # communicator with one rank (rollout -> PACK -> ncclAllReduce -> finalize from C)
     "c4_shard_native1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True, mode="rccl",
@@ -85,7 +90,7 @@ CPU_SHAPES = {
 }
 CPU_HEADLINE = {"arm_c3": "c3_arm_k4096_h32", "drone_c2": "c2_drone_k4096_h32",
                 "wholebody_c4": "c4r_wholebody_k4096_h64", "c4": "c4r_wholebody_k4096_h64",
-                "fleet_c5": "c4r_wholebody_k4096_h64"}
+                "fleet_c5": "c4r_wholebody_k4096_h64", "fleet_c5_share": "c4r_wholebody_k4096_h64"}
 
 
 def log(*a):
@@ -102,6 +107,8 @@ def build_info():
 
 
 def make_state(model: str, V: int) -> np.ndarray:
+    """Synthetic state rows of a fleet of V vehicles (row v = fleet-wide vehicle v: a vehicle-sharded
+    rank takes its own rows of the whole fleet's array)."""
     rng = np.random.default_rng(0)
     rows = []
     for v in range(V):
@@ -119,14 +126,17 @@ def make_state(model: str, V: int) -> np.ndarray:
     return np.asarray(rows, np.float64)
 
 
-def set_targets(eng, model, V):
+def set_targets(eng, model, vehicles):
+    """Targets of the fleet-wide vehicles ``vehicles`` (a range), set on the engine's vehicles 0..n-1."""
     rng = np.random.default_rng(1)
-    for v in range(V):
+    for v in range(vehicles.stop):
+        p = np.array(ARM_TARGET[0]) + (rng.uniform(-0.1, 0.1, 3) if v else 0.0)   # drawn for every v, in order
+        if v not in vehicles:
+            continue
         if model in ("drone", "quadrotor"):
-            eng.set_target(DRONE_TARGET, vehicle=v)
+            eng.set_target(DRONE_TARGET, vehicle=v - vehicles.start)
         else:   # targets jittered by +-0.1 m for v > 0 (SURVEY §8d C5)
-            p = np.array(ARM_TARGET[0]) + (rng.uniform(-0.1, 0.1, 3) if v else 0.0)
-            eng.set_target(p, ARM_TARGET[1], vehicle=v)
+            eng.set_target(p, ARM_TARGET[1], vehicle=v - vehicles.start)
 
 
 def shape_key(model: str, K: int, H: int, V: int = 1) -> str:
@@ -280,7 +290,28 @@ def timed_batches(run, n_batches, barrier, prime=None):
     return out, enq
 
 
-def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1):
+def latency_at_rate(se, state, calls: int, period_s: float = 0.01, idle_s: float = 0.1):
+    """Control calls at the node's cadence: the arm node ticks at 100 Hz (kinova.py:101,
+    rospy.Rate(100)), so between calls the GPU idles ~10 ms and its clocks drop (profiles/r04/ramp).
+    After ``idle_s`` of idle (no heat-up), ``calls`` control calls, each started on the next
+    ``period_s`` tick as rospy.Rate.sleep does; host-inclusive wall time per call."""
+    time.sleep(idle_s)
+    lat = []
+    nxt = time.perf_counter()
+    for _ in range(calls):
+        t1 = time.perf_counter()
+        se.step(state)
+        lat.append(time.perf_counter() - t1)
+        nxt += period_s
+        d = nxt - time.perf_counter()
+        if d > 0:
+            time.sleep(d)
+        else:   # (a call longer than the period: the next tick starts now)
+            nxt = time.perf_counter()
+    return lat
+
+
+def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1, lat_rate_calls=0):
     import torch
     from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
     w = dict(WORKLOADS[name])
@@ -288,21 +319,21 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     strong = w.pop("strong", False)
     force_native = w.pop("native", None)
     mode = w.pop("mode", None)
-    if strong:
+    if strong and mode != "vehicles":   # (a vehicle-split fleet: ShardedEngine splits the vehicles)
         if w["n_samples"] % world:
             raise SystemExit(f"{name}: K={w['n_samples']} does not split over {world} ranks")
         w["n_samples"] //= world
-    V = w.get("n_vehicles", 1)
     native = force_native if force_native is not None else (
         None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False)
     se = ShardedEngine(seed=1234, native=native, mode=mode, **w)
     eng = se.engine
-    set_targets(eng, w["model"], V)
+    V = eng.V   # this rank's vehicles (the fleet-wide ones: se.vehicles)
+    set_targets(eng, w["model"], se.vehicles)
     if w["model"] == "quadrotor":   # warm start at hover thrust (quadrotor_mppi.MPPI does the same)
         u = np.zeros((V, eng.H, eng.A), np.float32)
         u[..., 0] = eng.cfg.quad_mass * eng.cfg.quad_gravity
         eng.set_u_prev(u)
-    state = make_state(w["model"], V)
+    state = make_state(w["model"], se.vehicles.stop)[se.vehicles.start:]
     eng.set_state(state)
     red_dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else "cpu"
 
@@ -312,9 +343,14 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         # device, which it now spends while the batch still runs; eng.synchronize() then waits
         # for the batch's completion signal.  Both still bracket every batch.
         torch.cuda.synchronize()
-        eng.synchronize()
+        # on a multi-rank peer exchange se.synchronize() is itself a collective: the ranks agree that
+        # no step was given up (a MAX all-reduce, which doubles as the barrier); a timeout would have
+        # resynchronised the ranks and voids the measurement
+        if se.synchronize():
+            raise RuntimeError(f"{name}: a peer-exchange step timed out (ranks resynchronised): no valid timing")
         if dist is not None:
-            dist.barrier()
+            if se.mode != "peer":
+                dist.barrier()
             torch.cuda.synchronize()
 
     se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
@@ -379,14 +415,15 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         if i >= 20:
             lat.append(time.perf_counter() - t1)
     eng.synchronize()
-    if not lat:
+    lat100 = latency_at_rate(se, state, lat_rate_calls) if lat_rate_calls else []
+    if not lat and not lat100:
         se.step(state)
     dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
     out, u0, st = eng.read_outputs()
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.mode == "rccl" else None
-    res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat,
+    res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
            "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
            "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
@@ -495,6 +532,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                             "max over ranks; the same batches without the heat-up: ms_per_step_no_heatup"},
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
         "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
+        "latency_100hz": latency_100hz(r.get("lat100"), lat),
         "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
         "roofline": rf,
         "cpu_baseline": cpu,
@@ -513,12 +551,28 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                                    "IPC-mapped exchange region over xGMI and combine them from their own)",
                            "rccl": "engine-owned RCCL communicator: ncclAllReduce(SUM) of zero-padded "
                                    "partial-record slots",
-                           "torch": f"torch.distributed ({r['backend']}) all_reduce(SUM) of the slots"}[r["exchange"]],
+                           "torch": f"torch.distributed ({r['backend']}) all_reduce(SUM) of the slots",
+                           "vehicles": "none: the fleet's vehicles split over the ranks (each rank a whole "
+                                       "controller of its vehicles), nothing exchanged"}[r["exchange"]],
             "allreduce_us": tim.get("allreduce_us") if tim else None,
             "native_comm_error": r["native_error"],
             "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
             "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
     return line
+
+
+def latency_100hz(lat100, lat_b2b):
+    """The control call at the node's 100 Hz cadence (latency_at_rate) beside the back-to-back one."""
+    if not lat100:
+        return None
+    x = np.array(lat100) * 1e3
+    p50 = float(np.median(x))
+    b2b = float(np.median(lat_b2b)) if len(lat_b2b) else None
+    return {"p50_ms": p50, "p99_ms": float(np.percentile(x, 99)), "mean_ms": float(x.mean()), "calls": int(x.size),
+            "period_ms": 10.0, "vs_back_to_back_p50": p50 / b2b if b2b else None,
+            "what": "host-inclusive control call (state in, outputs, check_reach) started on every 10 ms tick after "
+                    "100 ms idle, no heat-up: the arm node's rospy.Rate(100) loop (kinova.py:101); the GPU idles "
+                    "~10 ms between calls"}
 
 
 def secondary_entry(s, ns):
@@ -539,6 +593,9 @@ def secondary_entry(s, ns):
     if s["world"] > 1:
         e.update({"exchange": s["exchange"], "native_comm_error": s["native_error"],
                   "rollout_us_max_over_ranks": s["tim"].get("rollout_in_step_us_max_over_ranks")})
+    if s.get("exchange") == "vehicles":   # the fleet split over the ranks: no exchange at all
+        e.update({"exchange": "none", "split": "vehicles", "vehicles_total": s["world"] * s["V"], "samples_total": s["K"],
+                  "vehicles_per_gpu": s["V"], "allreduce_us": None})
     return e
 
 
@@ -586,9 +643,10 @@ def main():
                          "control steps); no roofline in the line")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="leave the process's CPU affinity alone (default: bind to the GPU's local CPUs)")
-    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4_shard_peer1,c4,fleet_c5,quadrotor_c2",
+    ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4_shard_peer1,c4,fleet_c5,"
+                                           "fleet_c5_share,quadrotor_c2",
                     help="extra workloads reported at N=1, comma separated; '' for none")
-    ap.add_argument("--secondary-multi", default="c4",
+    ap.add_argument("--secondary-multi", default="c4,fleet_c5",
                     help="extra workloads reported at N>1 (every rank runs them), comma separated; '' for none")
     args = ap.parse_args()
     # the JSON line is the only thing on stdout: keep the real stdout for it and send fd 1 to
@@ -633,7 +691,7 @@ def main():
         WORKLOADS[workload] = dict(WORKLOADS[workload], n_samples=args.samples, strong=False)
     batches = args.batches or auto_batches(args.steps)
     r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
-                     timing=not args.no_kernel_timing, batches=batches)
+                     timing=not args.no_kernel_timing, batches=batches, lat_rate_calls=args.latency_steps)
     secondary = {}
     extra = args.secondary if world == 1 else args.secondary_multi
     if extra and r["tim"] is not None:

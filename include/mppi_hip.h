@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 6
+#define MPPI_ABI_VERSION 7
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_PEER_HANDLE_BYTES 64  /* hipIpcMemHandle_t */
 #define MPPI_MAX_ACTION 16
@@ -55,7 +55,9 @@ typedef enum {
     MPPI_ERR_HIP = -2,
     MPPI_ERR_NONFINITE = -3,
     MPPI_ERR_STATE = -4,
-    MPPI_ERR_COMM = -5
+    MPPI_ERR_COMM = -5,
+    MPPI_ERR_PEER_TIMEOUT = -6  /* mppi_synchronize: a peer-exchange step was given up since the last
+                                   mppi_peer_reset (the engine itself is fine; see mppi_peer_status) */
 } mppi_status;
 
 /* Rollout models.  A = action dimension. */
@@ -143,6 +145,10 @@ typedef struct {
     int32_t quad_literal_jinv;  /* 1: steps t >= 1 integrate rpy += dt inv(J(rpy)) omega exactly as
                                  * the commented loop (drone_mppi.py:73-76); 0 (default): J at
                                  * every step (J maps body rates to Euler rates, drone.py:114-124) */
+    int32_t vehicle_offset;     /* fleet-wide index of this engine's vehicle 0 (vehicle sharding, config C5:
+                                 * each GPU runs V of the fleet's vehicles).  The device noise is keyed by
+                                 * the fleet-wide index, so an engine over vehicles [o, o+V) draws exactly
+                                 * what one engine over the whole fleet draws for them.  0..32767-V */
 } mppi_config;
 
 typedef enum {
@@ -207,8 +213,12 @@ mppi_status mppi_get_u_prev(mppi_engine* e, float* u_prev);
  * Async host->device (pinned staging) on the engine stream. */
 mppi_status mppi_set_state(mppi_engine* e, const double* state);
 
-/* Step counter used as the Philox counter word (device resident). */
+/* Step counter used as the Philox counter word (device resident).  On an engine connected by the
+ * peer exchange it also moves the exchange epoch carried in the tags (every rank must call it the
+ * same number of times, like the steps themselves): words left in the regions under the old
+ * counter then never pass for a later step's. */
 mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step);
+mppi_status mppi_get_step_counter(mppi_engine* e, uint32_t* step);
 
 /* Split-phase step (async, stream ordered).  d_noise: device eps (V,K,H,A) in
  * INJECTED mode, else NULL.  With shard_count > 1 either bind a zero-initialised
@@ -256,9 +266,19 @@ mppi_status mppi_exchange(mppi_engine* e);
  * partials (its own from registers, the others from its own region once all their tags are the
  * step's): a control step is the unsharded step's two kernels (native dispatch included), no
  * PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
- * rank reproduces the unsharded engine exactly.  A block that waits 2 s for a peer gives up:
- * the step keeps the warm start (w_eps = 0) and reports stats nonfinite = 2, so a rank that
- * stopped cannot hang or poison the others.
+ * rank reproduces the unsharded engine exactly.
+ * Failure handling.  A block that waits 2 s for a peer gives the step up: the step keeps the warm
+ * start (w_eps = 0), and the block reports the timeout three ways -- into the control word of this
+ * rank in EVERY rank's region, as the step's abort tag over its header words in the peers' regions
+ * (a peer still polling that step gives it up too), and into this engine's sticky word.  From then
+ * on every rank's finalize blocks find the report in their own region and give every step up at
+ * once (u_prev held on every rank, no 2 s waits) until the host resets the exchange, so no rank
+ * keeps updating a warm start the others did not.  The host sees it as stats nonfinite = 2 from
+ * mppi_read_outputs (this step's flag on any dim, or the sticky word: any block of any step of a
+ * batch), as MPPI_ERR_PEER_TIMEOUT from mppi_synchronize, and through mppi_peer_status (this rank's
+ * sticky word and every rank's report as stored in this rank's region).  Recovery is collective
+ * (distributed.py ShardedEngine.resync): agree over the process group, take rank 0's warm start,
+ * step counter and epoch, and call mppi_peer_reset on every rank between two barriers.
  * Every rank must run the same sequence of steps with the same step counter (the tags are the
  * Philox counter): a rank that skips a step or rewinds its counter alone leaves the others
  * waiting out the 2 s bound.  mppi_get_weighted_noise gathers the last exchanged step's
@@ -281,6 +301,15 @@ mppi_status mppi_peer_connect_ptrs(mppi_engine* e, const uint64_t* device_addres
  * finalize's own tagged stores and polls over the regions in a one-wave kernel (every rank's word
  * within 2 s, else MPPI_ERR_COMM) and clears the region again. */
 mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase);
+/* The exchange's failure state: sticky = this engine's timeout word (the given-up step's tag, 0 =
+ * none; host memory, no device access); reports (kMaxPeers = 8 words, may be NULL) = the timeout
+ * reports in this rank's region, word r from rank r (tag << 32 | 1, 0 = none; a device-to-host copy
+ * after the engine's work); epoch (may be NULL) = the exchange epoch of the tags. */
+mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports, uint32_t* epoch);
+/* Collective recovery after a timeout: with every rank's engine synchronised and a barrier passed
+ * (no kernel writes into any region), clear this rank's region and sticky word and take the step
+ * counter and epoch the ranks agreed on; a second barrier follows before any rank steps again. */
+mppi_status mppi_peer_reset(mppi_engine* e, uint32_t step, uint32_t epoch);
 
 /* Synchronise and copy the step's outputs: out (V, output_dim) doubles
  *   DRONE: x_des(3) v_des(3);  ARM: qdes(nq) vdes(nq);  WHOLEBODY: x(3) v(3) qdes(nq) vdes(nq)

@@ -19,9 +19,10 @@ MAX_ACTION, MAX_JOINTS, MAX_HORIZON, MAX_SAVGOL = 16, 16, 256, 31
 MODEL_DRONE, MODEL_ARM, MODEL_WHOLEBODY, MODEL_QUADROTOR = 0, 1, 2, 3
 NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
-OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
+OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM, ERR_PEER_TIMEOUT = 0, -1, -2, -3, -4, -5, -6
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 6
+ABI_VERSION = 7
+MAX_PEERS = 8
 COMM_ID_BYTES = 128
 PEER_HANDLE_BYTES = 64
 
@@ -51,7 +52,8 @@ class Config(C.Structure):
                 ("q_center", C.c_float * MAX_JOINTS), ("q_lower", C.c_float * MAX_JOINTS),
                 ("q_upper", C.c_float * MAX_JOINTS),
                 ("quad_mass", C.c_float), ("quad_inertia", C.c_float * 3), ("quad_kd", C.c_float),
-                ("quad_gravity", C.c_float), ("quad_literal_jinv", C.c_int32)]
+                ("quad_gravity", C.c_float), ("quad_literal_jinv", C.c_int32),
+                ("vehicle_offset", C.c_int32)]
 
 
 class Link(C.Structure):
@@ -92,6 +94,7 @@ PROTOTYPES = {
     "mppi_get_u_prev": (_ST, [_P, _F]),
     "mppi_set_state": (_ST, [_P, _D]),
     "mppi_set_step_counter": (_ST, [_P, C.c_uint32]),
+    "mppi_get_step_counter": (_ST, [_P, _U32]),
     "mppi_exchange_slot_floats": (_ST, [_P, _I64]),
     "mppi_bind_exchange": (_ST, [_P, _P]),
     "mppi_rollout": (_ST, [_P, _P]),
@@ -105,6 +108,8 @@ PROTOTYPES = {
     "mppi_peer_probe": (_ST, [_P, C.c_int32]),
     "mppi_peer_region": (_ST, [_P, C.POINTER(C.c_uint64)]),
     "mppi_peer_connect_ptrs": (_ST, [_P, C.POINTER(C.c_uint64)]),
+    "mppi_peer_status": (_ST, [_P, _U32, C.POINTER(C.c_uint64), _U32]),
+    "mppi_peer_reset": (_ST, [_P, C.c_uint32, C.c_uint32]),
     "mppi_comm_info": (_ST, [_P, _I32, _I32]),
     "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),
@@ -149,6 +154,11 @@ class MPPIError(RuntimeError):
         self.status = status
 
 
+class PeerTimeout(MPPIError):
+    """MPPI_ERR_PEER_TIMEOUT: a peer-exchange step was given up since the last reset (the engine
+    still works; every rank holds its warm start until ShardedEngine.resync / mppi_peer_reset)."""
+
+
 def lib():
     """Load libmppi_hip.so (once).  Raises if it is missing -- no CPU fallback."""
     global _lib
@@ -190,7 +200,7 @@ def lib():
 def check(status: int, what: str = "") -> None:
     if status != OK:
         msg = lib().mppi_last_error().decode(errors="replace")
-        raise MPPIError(status, f"{what}: {msg}" if what else msg)
+        raise (PeerTimeout if status == ERR_PEER_TIMEOUT else MPPIError)(status, f"{what}: {msg}" if what else msg)
 
 
 def fptr(a):

@@ -381,6 +381,8 @@ struct mppi_engine {
     size_t x_bytes = 0;
     std::vector<void*> x_opened;        // the other ranks' regions, IPC-mapped
     unsigned long long** d_xpeers = nullptr;   // (shard_count) region pointers, device resident
+    uint32_t x_epoch = 0;               // the exchange epoch in the tags (mppi_dev.h peer_tag): moved by
+                                        // mppi_set_step_counter and mppi_peer_reset on a connected engine
     VehicleConst* h_vc = nullptr;       // pinned staging
     unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
     unsigned char* h_out_dev = nullptr; // device view of h_out
@@ -429,7 +431,7 @@ FinTail tail_of(const FinParams& f, int32_t mode) {
     t.u_prev = f.u_prev; t.vc = f.vc;
     t.out = f.out; t.u0 = f.u0; t.stats = f.stats; t.flags = f.flags; t.wraw = f.wraw; t.wsmooth = f.wsmooth;
     t.dst = f.dst; t.xbase = f.xbase; t.xslot = f.xslot; t.nslots = f.nslots; t.myslot = f.myslot; t.P = f.P;
-    t.xpeers = f.xpeers; t.xlocal = f.xlocal; t.xn = f.xn; t.xme = f.xme;
+    t.xpeers = f.xpeers; t.xlocal = f.xlocal; t.xn = f.xn; t.xme = f.xme; t.xerr = f.xerr;
     std::memcpy(t.sg, f.sg, sizeof(t.sg));
     return t;
 }
@@ -490,6 +492,14 @@ size_t off_stats(const mppi_engine* e) { return (off_u0(e) + (size_t)e->V * e->A
 // the host polls their tags and takes the values from the records themselves
 size_t off_flags(const mppi_engine* e) { return off_stats(e) + (size_t)e->V * 16; }
 size_t rec_count(const mppi_engine* e) { return (size_t)e->V * (2 * e->A + 1); }
+// the peer exchange's sticky timeout word (16 B after the records): the step tag of a finalize
+// block that gave a step up, written by that block, cleared only by the host (mppi_peer_reset)
+size_t off_xerr(const mppi_engine* e) { return off_flags(e) + rec_count(e) * 16; }
+uint32_t sticky_timeout(const mppi_engine* e) {
+    return e->h_out ? *(const volatile uint32_t*)(e->h_out + off_xerr(e)) : 0u;
+}
+// this rank's exchange region past its control words (mppi_dev.h kXCtl): the partials' base
+unsigned long long* xdata(const mppi_engine* e) { return e->d_xregion + kXCtl; }
 
 mppi_status build_vehicle_consts(mppi_engine* e) {
     const mppi_config& c = e->cfg;
@@ -499,6 +509,7 @@ mppi_status build_vehicle_consts(mppi_engine* e) {
         for (int j = 0; j < kMaxJ; ++j) { vc.qc[j] = c.q_center[j]; vc.qlo[j] = c.q_lower[j]; vc.qhi[j] = c.q_upper[j]; }
         const double* s = e->state.data() + (size_t)v * e->state_dim;
         std::memcpy(vc.tpos, &e->tpos[3 * v], 3 * sizeof(float));
+        std::memcpy(&vc._pad[2], &e->x_epoch, sizeof(uint32_t));   // the exchange epoch (kVcEpochWord)
         quat_xyzw_to_R(&e->tquat[4 * v], vc.tR);
         if (c.model == MPPI_MODEL_DRONE) {
             for (int a = 0; a < 3; ++a) {
@@ -649,6 +660,9 @@ mppi_status validate(const mppi_config& c) {
     if (!(c.lambda_ > 0.0) || !(c.dt > 0.0)) return fail(MPPI_ERR_INVALID_ARG, "lambda and dt must be > 0");
     if (c.shard_count < 1 || c.shard_rank < 0 || c.shard_rank >= c.shard_count)
         return fail(MPPI_ERR_INVALID_ARG, "shard %d/%d", c.shard_rank, c.shard_count);
+    if (c.vehicle_offset < 0 || c.vehicle_offset + c.n_vehicles > 32768)
+        return fail(MPPI_ERR_INVALID_ARG, "vehicle_offset %d: the fleet-wide vehicle index must stay below 32768",
+                    c.vehicle_offset);
     if (c.cost_terms & ~0x1F) return fail(MPPI_ERR_INVALID_ARG, "unknown cost_terms bits 0x%x", c.cost_terms);
     if (c.cost_terms && (c.model == MPPI_MODEL_DRONE || c.model == MPPI_MODEL_QUADROTOR))
         return fail(MPPI_ERR_INVALID_ARG, "cost_terms apply to the ARM / WHOLEBODY CostManager (not DRONE)");
@@ -838,7 +852,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     int iters = (groups + nb - 1) / nb;
     // a block's cost run (iters * nw * R samples) is staged in LDS for one write-through store
     // (k_rollout): at most kMaxCostRun floats, more blocks otherwise
-    iters = std::min(iters, std::max(1, kMaxCostRun / (nw * R)));
+    iters = std::min(iters, std::max(1, kMaxCostRun / cost_run_stride(nw * R)));
     nb = (groups + iters - 1) / iters;
     if (c.model == MPPI_MODEL_QUADROTOR) {   // k_rollout_quad: 16 rollouts (4 lanes each) per dynamics
         e->threads = 256;                     // wave; 1 dynamics wave per block up to 1024 blocks, else 4
@@ -894,7 +908,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
     if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * traj_floats(e)));
     if (c.store_noise) CREATE_TRY(hipMalloc(&e->d_noise_out, sizeof(float) * KH * e->A));
-    e->out_bytes = (int64_t)(off_flags(e) + rec_count(e) * 16);
+    e->out_bytes = (int64_t)(off_xerr(e) + 16);
     CREATE_TRY(hipMalloc(&e->d_out, e->out_bytes));
     CREATE_TRY(hipHostMalloc((void**)&e->h_out, e->out_bytes, hipHostMallocMapped | hipHostMallocCoherent));
     CREATE_TRY(hipHostGetDevicePointer((void**)&e->h_out_dev, e->h_out, 0));
@@ -956,7 +970,8 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     p.model = c.model; p.V = e->V; p.K = e->K; p.H = H; p.A = e->A;
     p.L = L; p.R = R; p.nch = nch; p.nb = nb; p.iters = iters;
     p.nq = e->nq; p.qoff = e->qoff; p.nj = c.n_joints;
-    p.noise_mode = c.noise_mode; p.state_f64 = c.state_f64;
+    // (the vehicle offset in the high half: the rollouts' fleet-wide Philox vehicle key)
+    p.noise_mode = c.noise_mode | (c.vehicle_offset << 16); p.state_f64 = c.state_f64;
     p.store_traj = c.store_trajectory; p.store_noise = c.store_noise;
     bool diag = true;
     for (int a = 0; a < e->A; ++a)
@@ -1027,6 +1042,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     f.u0 = (float*)(e->h_out_dev + off_u0(e));
     f.stats = (float*)(e->h_out_dev + off_stats(e));
     f.flags = (uint32_t*)(e->h_out_dev + off_flags(e));
+    f.xerr = (uint32_t*)(e->h_out_dev + off_xerr(e));
     f.wraw = e->d_wraw; f.wsmooth = e->d_wsmooth; f.out_dim = e->out_dim;
     if (const char* dbg = getenv("MPPI_FIN_DEBUG")) f.dbg = atoi(dbg);
     e->event_wait = getenv("MPPI_EVENT_WAIT") && atoi(getenv("MPPI_EVENT_WAIT")) != 0;
@@ -1045,6 +1061,7 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
         t[kTailScratch].u0 = (float*)(e->d_out + off_u0(e));
         t[kTailScratch].stats = (float*)(e->d_out + off_stats(e));
         t[kTailScratch].flags = (uint32_t*)(e->d_out + off_flags(e));
+        t[kTailScratch].xerr = (uint32_t*)(e->d_out + off_xerr(e));
         t[kTailScratch].wraw = nullptr;
         t[kTailScratch].wsmooth = nullptr;
         // the step's FINAL stores no readback copies of w_eps: mppi_get_weighted_noise recomputes
@@ -1161,6 +1178,16 @@ mppi_status mppi_set_step_counter(mppi_engine* e, uint32_t step) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
     if (use_device(e)) return MPPI_ERR_HIP;
     e->step_ctr = step;
+    if (e->peer) {   // a new exchange epoch: words left in the regions under the old counter never match
+        ++e->x_epoch;
+        return build_vehicle_consts(e);   // (V == 1: the constants ride in the kernel arguments)
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_step_counter(mppi_engine* e, uint32_t* step) {
+    if (!e || !step) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    *step = e->step_ctr;
     return MPPI_OK;
 }
 
@@ -1307,7 +1334,7 @@ mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
     if (e->comm || e->d_exchange) return fail(MPPI_ERR_STATE, "peer exchange: the engine already has an exchange");
     if (e->d_xregion) return fail(MPPI_ERR_STATE, "peer exchange: region already open");
     if (use_device(e)) return MPPI_ERR_HIP;
-    const size_t bytes = 2 * (size_t)e->cfg.shard_count * fin_blocks(e) * kXW * sizeof(unsigned long long);
+    const size_t bytes = (kXCtl + 2 * (size_t)e->cfg.shard_count * fin_blocks(e) * kXW) * sizeof(unsigned long long);
     // uncached: the words other GPUs store into it are never behind a stale line of this GPU's L2
     void* p = nullptr;
     hipError_t r = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
@@ -1317,7 +1344,7 @@ mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
     }
     e->d_xregion = (unsigned long long*)p;
     e->x_bytes = bytes;
-    HIP_TRY(hipMemset(p, 0, bytes));   // tags 0: no step's (bit 31 is set in every tag)
+    HIP_TRY(hipMemset(p, 0, bytes));   // tags 0: no step's (bit 31 is set in every tag); no timeout reports
     hipIpcMemHandle_t h;
     static_assert(sizeof(h) == MPPI_PEER_HANDLE_BYTES, "hipIpcMemHandle_t size");
     HIP_TRY(hipIpcGetMemHandle(&h, p));
@@ -1325,13 +1352,15 @@ mppi_status mppi_peer_open(mppi_engine* e, uint8_t* handle) {
     return MPPI_OK;
 }
 
-// the regions' device addresses, in rank order, into the finalize's tail (both connects)
-static mppi_status peer_bind(mppi_engine* e, const std::vector<unsigned long long*>& ptrs) {
+// the regions' device addresses (past their control words), in rank order, into the finalize's
+// tail (both connects)
+static mppi_status peer_bind(mppi_engine* e, std::vector<unsigned long long*> ptrs) {
     const int n = e->cfg.shard_count, me = e->cfg.shard_rank;
+    for (auto& p : ptrs) p += kXCtl;
     if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
     HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
     FinParams& f = e->fp;
-    f.xpeers = e->d_xpeers; f.xlocal = e->d_xregion; f.xn = n; f.xme = me;
+    f.xpeers = e->d_xpeers; f.xlocal = xdata(e); f.xn = n; f.xme = me;
     FinTail t[2] = {tail_of(f, 0), tail_of(f, 2)};
     t[0].wraw = t[0].wsmooth = nullptr;   // (as at create: the step's FINAL stores no readback copies)
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1404,7 +1433,7 @@ mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase) {
         unsigned long long* d_got = nullptr;
         HIP_TRY(hipMalloc(&d_got, kMaxPeers * sizeof(unsigned long long)));
         const uint32_t tag = 0x3C3C0000u;   // (bit 31 clear: never a step's tag)
-        int rc = mppi_launch_peer_probe(e->d_xpeers, e->d_xregion, n, me, slot, tag, kPeerWaitTicks, d_got, e->stream);
+        int rc = mppi_launch_peer_probe(e->d_xpeers, xdata(e), n, me, slot, tag, kPeerWaitTicks, d_got, e->stream);
         std::vector<unsigned long long> got(kMaxPeers, 0ull);
         hipError_t he = rc == 0 ? hipStreamSynchronize(e->stream) : (hipError_t)rc;
         if (he == hipSuccess) he = hipMemcpy(got.data(), d_got, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
@@ -1430,13 +1459,47 @@ mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase) {
     }
     std::vector<unsigned long long> got(n);
     for (int r = 0; r < n; ++r)
-        HIP_TRY(hipMemcpy(&got[r], e->d_xregion + (size_t)r * slot, sizeof(got[r]), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&got[r], xdata(e) + (size_t)r * slot, sizeof(got[r]), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
     HIP_TRY(hipDeviceSynchronize());
     for (int r = 0; r < n; ++r)
         if (got[r] != pattern(r, me))
             return fail(MPPI_ERR_COMM, "peer exchange: rank %d's probe word did not arrive (%016llx)", r, got[r]);
     return MPPI_OK;
+}
+
+// The exchange's failure state.  sticky: this engine's own timeout word (a step tag, 0 = none;
+// mapped host memory, no device access).  reports (may be NULL): the control words of this rank's
+// region, one per rank (a step tag << 32 | 1 from every rank that gave a step up since the last
+// reset; a device-to-host copy of kMaxPeers words, after waiting for the engine's work).
+mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports, uint32_t* epoch) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_status before mppi_peer_open");
+    if (reports) {
+        if (use_device(e)) return MPPI_ERR_HIP;
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(hipMemcpy(reports, e->d_xregion, kMaxPeers * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    if (sticky) *sticky = sticky_timeout(e);
+    if (epoch) *epoch = e->x_epoch;
+    return MPPI_OK;
+}
+
+// Collective recovery after a timeout (distributed.py ShardedEngine.resync): every rank has
+// synchronised its engine and passed a barrier, so no kernel writes into any region; each rank
+// clears its own region (partials and timeout reports) and its sticky word, and takes the step
+// counter and exchange epoch every rank agreed on; a second barrier follows before any rank steps.
+mppi_status mppi_peer_reset(mppi_engine* e, uint32_t step, uint32_t epoch) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->peer) return fail(MPPI_ERR_STATE, "mppi_peer_reset before mppi_peer_connect");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
+    HIP_TRY(hipDeviceSynchronize());
+    *(volatile uint32_t*)(e->h_out + off_xerr(e)) = 0u;
+    e->step_ctr = step;
+    e->x_epoch = epoch;
+    return build_vehicle_consts(e);
 }
 
 // the rollout's per-block partial records (DevParams::hdr / rdata layout)
@@ -1609,7 +1672,13 @@ static mppi_status assemble_records(mppi_engine* e) {
             std::memcpy(&e->rec_u0[(size_t)v * A + a], &w[2], 4);
             if (!load_record(e, r0 + 2 * a + 1, want, w)) return fail(MPPI_ERR_STATE, "output record (%d,%d) not tagged", v, a);
             std::memcpy(&o2, w, 8);
-            if (a == 0) std::memcpy(&e->rec_stats[(size_t)v * 4 + 3], &w[2], 4);
+            {   // the step's nan / exchange-timeout flag: the largest over every dim's record (a
+                // peer-exchange block that gave the step up flags its own dim: any dim counts)
+                float nf;
+                std::memcpy(&nf, &w[2], 4);
+                float& st3 = e->rec_stats[(size_t)v * 4 + 3];
+                st3 = (a == 0 || nf > st3 || std::isnan(nf)) ? nf : st3;
+            }
             double* ov = e->rec_out.data() + (size_t)v * od;
             if (model == MPPI_MODEL_QUADROTOR) continue;
             if (model == MPPI_MODEL_DRONE || (model == MPPI_MODEL_WHOLEBODY && a < 3)) {
@@ -1680,8 +1749,9 @@ mppi_status mppi_read_outputs(mppi_engine* e, double* out, float* u0, mppi_stats
                               std::fabs(T16[11] - e->tpos[3 * v + 2]);
             reach = err < e->cfg.reach_tol;
         }
-        // 2: a peer-exchange step that waited out its bound for another rank (it kept u_prev)
-        const int nf = (st[4 * v + 3] >= 2.0f) ? 2
+        // 2: a peer-exchange step given up (a rank's timeout: u_prev kept) -- this step's flag or
+        // any step's since the exchange was last reset (the sticky word: every block, every step)
+        const int nf = (st[4 * v + 3] >= 2.0f || (e->peer && sticky_timeout(e) != 0u)) ? 2
                        : ((st[4 * v + 3] > 0.0f) || !std::isfinite(st[4 * v]) || !std::isfinite(uu[(size_t)v * e->A]));
         nonfinite |= nf;
         if (stats) {
@@ -2119,6 +2189,10 @@ mppi_status mppi_synchronize(mppi_engine* e) {
         if (st != MPPI_OK) return st;
     }
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->peer)
+        if (const uint32_t t = sticky_timeout(e))
+            return fail(MPPI_ERR_PEER_TIMEOUT, "peer exchange: a step was given up (tag %08x): this rank's "
+                                               "warm start may differ from its peers' until mppi_peer_reset", t);
     return MPPI_OK;
 }
 

@@ -15,6 +15,9 @@ constexpr int kHdr = 4;  // partial record header: rho, eta, eta2, pad
 // k_rollout stages a block's costs (iters x waves x rollouts per wave consecutive samples) in LDS
 // for one write-through store run; create keeps the run within this many floats (16 KB)
 constexpr int kMaxCostRun = 4096;
+// one group's run of costs in that stage (nS = waves x rollouts per wave floats), padded to 16 B
+// so every run starts 16 B aligned for st_dev_run's b128 LDS reads
+constexpr inline int cost_run_stride(int nS) { return (nS + 3) & ~3; }
 
 // One joint of the chain, pre-baked on the host exactly the way the reference
 // builds its tensors (transformation_matrix.py:28-35, 58-95).
@@ -41,7 +44,9 @@ struct VehicleConst {
                           //      fixed joints; column 3 = R * (their translation), p(k,t) is added
     float tpos[3];        // target position
     float tR[9];          // target rotation (quaternion_to_matrix, xyzw)
-    float _pad[4];        // [0]: a native control call's sequence number (bits; k_finalize, kSeqFromVc)
+    float _pad[4];        // [0]: a native control call's sequence number (bits; k_finalize, kSeqFromVc);
+                          // [1]: the step's Philox counter (written by the rollout, kVcStepWord);
+                          // [2]: the peer exchange's epoch (host-set, kVcEpochWord)
     float qc[kMaxJ];      // extra cost terms (mppi_config): centering target and joint limits
     float qlo[kMaxJ];     //   per arm joint (the same for every vehicle)
     float qhi[kMaxJ];     // sizeof = 688 (16-byte multiple: keeps the dynamic LDS base aligned)
@@ -145,6 +150,7 @@ struct FinTail {
     unsigned long long* const* xpeers;   // peer exchange (mppi_peer_connect): every rank's region, null = off
     unsigned long long* xlocal;          //   this rank's region (the ranks' partials are gathered from it)
     int32_t xn, xme;                     //   rank count, this rank
+    uint32_t* xerr;                      //   sticky timeout word (mapped host memory; read on the late path only)
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
@@ -156,12 +162,30 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // every k_finalize block pushes its partial -- header (rho, eta, eta2, nan) and its window's
 // columns N[t] -- into every rank's exchange region, and gathers the ranks' partials of the same
 // block from its own.  Each word is 8 B, (value bits, tag): one store carries its own validity,
-// so nothing is ordered against anything else.  Region: [2 step parities][ranks][V*grid.x blocks]
-// [kXW words].  The tag is the step's Philox counter with bit 31 set, which the rollout's block 0
-// hands to the finalize in the vehicle constants (word kVcStepWord).
+// so nothing is ordered against anything else.  Region: [kXCtl control words] then [2 step
+// parities][ranks][V*grid.x blocks][kXW words]; the ranks' region pointers (FinTail::xpeers,
+// xlocal) point past the control words.  Control word r is rank r's timeout report: any of its
+// finalize blocks that gives up a step stores (tag, 1) there in EVERY rank's region, and from then
+// on every rank's blocks find it in their own region and keep the warm start at once ("broken"
+// until the host resets the exchange, mppi_peer_reset): no rank goes on updating a warm start the
+// others did not.
+// The tag (peer_tag) is bit 31 | the exchange epoch (10 bits) | the step's Philox counter (low 20
+// bits).  The rollout's block 0 hands the counter to the finalize in the vehicle constants (word
+// kVcStepWord); the host puts the epoch there (kVcEpochWord; mppi_set_step_counter and
+// mppi_peer_reset move it), so words a rank left in a region before its counter was rewound can
+// never pass for a later step's.  Bit 30 marks an abort: a block that gives up a step overwrites
+// its header words in the peers' regions with the step's abort tag, and a peer still polling that
+// step gives it up too.
 constexpr int kMaxPeers = 8;
 constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
+constexpr int kXCtl = 16;        // control words at the head of a region (8 B each; kMaxPeers used)
 constexpr int kVcStepWord = (int)(offsetof(VehicleConst, _pad) / 4) + 1;
+constexpr int kVcEpochWord = kVcStepWord + 1;
+constexpr uint32_t kTagValid = 0x80000000u, kTagAbort = 0x40000000u;
+// (constexpr: usable from host and device code alike)
+constexpr inline uint32_t peer_tag(uint32_t step, uint32_t epoch) {
+    return kTagValid | ((epoch & 0x3FFu) << 20) | (step & 0xFFFFFu);
+}
 // a finalize block waits at most this long for its peers' partials (s_memrealtime, 100 MHz), then
 // finalises with the nan flag set (2): a rank that stopped stepping cannot hang the others
 constexpr uint64_t kPeerWaitTicks = 200000000ull;   // 2 s
@@ -206,6 +230,7 @@ struct FinParams {
     unsigned long long* const* xpeers;   // peer exchange (FinTail): the ranks' regions, this rank's,
     unsigned long long* xlocal;          //   rank count, this rank; xpeers null = off
     int32_t xn, xme;
+    uint32_t* xerr;                      //   sticky timeout word (mapped host memory)
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

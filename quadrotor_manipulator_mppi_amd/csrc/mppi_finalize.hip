@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     unsigned long long xpl = 0ull;   // lane d < xn: rank d's region address (wave 0's stores read it by readlane)
     unsigned long long* xlocal = nullptr;
     int32_t xn = 0, xme = 0;
-    uint32_t xstep = 0u;
+    uint32_t xstep = 0u, xep = 0u;
     float sg[WIN > 0 ? WIN : 1];
     auto pin_tail = [&]() {
         // every load issues first, then two empty asms consume them (one wait): pinned one
@@ -184,7 +184,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             x0d = ld_dev(vcp->pos0 + a); v0d = ld_dev(vcp->vel0 + a);
             if (seq == kSeqFromVc) seqv = ld_dev((const uint32_t*)vcp->_pad);   // (its bits)
         }
-        if (tid == 0 && xpeers) xstep = ld_dev((const uint32_t*)(vcb + v) + kVcStepWord);   // the exchange's tag
+        if (tid == 0 && xpeers) {   // the exchange's tag: the step's counter and the exchange epoch
+            xstep = ld_dev((const uint32_t*)(vcb + v) + kVcStepWord);
+            xep = ld_dev((const uint32_t*)(vcb + v) + kVcEpochWord);
+        }
         // every rank's region address, one per lane, loaded here so it lands during the record fold:
         // loaded per rank inside the store loop, each pointer load's wait also waited for the
         // previous rank's system-scope stores to complete (vmcnt counts stores): G - 1 serial
@@ -301,23 +304,25 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // its tag is this step's, and all are combined in rank order (the same order on every rank: every rank finalises
         // bit-identically; one rank reproduces the unsharded step exactly, f = exp(0) = 1).
         const uint32_t step = __builtin_amdgcn_readfirstlane(xstep);
-        const uint32_t tag = step | 0x80000000u;
+        const uint32_t tag = peer_tag(step, __builtin_amdgcn_readfirstlane(xep)), atag = tag | kTagAbort;
         // (the grid from geo, not gridDim: that reads the hidden kernel arguments, which native
         // dispatch does not supply; V == 1 on a peer-exchange engine)
         const size_t nbk = (size_t)8 * na * ts, blk = blockIdx.x;
         const size_t par = step & 1u;
         const float hown = (lane == 0) ? rho : (lane == 1) ? eta : (lane == 2) ? eta2 : nanf;
+        const size_t off = ((par * (size_t)xn + (size_t)xme) * nbk + blk) * kXW;   // this block's slot
+        typedef __attribute__((address_space(1))) unsigned long long gst64;
+        auto region = [&](int d) {   // rank d's region (uniform: d is)
+            return (gst64*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(xpl >> 32), d) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)xpl, d));
+        };
         if (mode == 0) {   // (this rank's own partial stays in registers: no round trip through memory)
             const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
             const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
-            const size_t off = ((par * (size_t)xn + (size_t)xme) * nbk + blk) * kXW;
-            typedef __attribute__((address_space(1))) unsigned long long gst64;
 #pragma unroll
             for (int d = 0; d < kMaxPeers; ++d) {   // (uniform branches; no wait between the ranks' stores)
                 if (d >= xn || d == xme) continue;
-                const uint64_t pa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(xpl >> 32), d) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)xpl, d);
-                gst64* dst = (gst64*)pa + off;
+                gst64* dst = region(d) + off;
                 if (lane < W) __hip_atomic_store(dst + kHdr + lane, wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (lane < kHdr) __hip_atomic_store(dst + lane, wh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -339,6 +344,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         const bool needc = lane < W, needh = lane < kHdr;
         uint32_t pend = ((1u << xn) - 1u) & ~(1u << xme);   // (uniform)
         const unsigned long long* src = xlocal + (par * (size_t)xn * nbk + blk) * kXW;
+        gu64* const ctl = (gu64*)xlocal - kXCtl;   // the ranks' timeout reports (mppi_dev.h kXCtl)
         const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
         bool late = false;
         while (pend != 0u) {
@@ -354,6 +360,18 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                     xh[r] = __hip_atomic_load(s + (lane & (kHdr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
+            // (in the same batch of loads: lane r < xn reads rank r's timeout report)
+            const unsigned long long xk = __hip_atomic_load(ctl + (lane < xn ? lane : 0), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_SYSTEM);
+            // Any rank reported a timeout since the last reset, or a pending peer gave this very step
+            // up (its header words carry the step's abort tag): this step is given up too, at once.
+            // After one rank's timeout every rank keeps its warm start until the host resets the
+            // exchange, so no rank goes on updating a warm start the others did not.
+            uint64_t bad = __builtin_amdgcn_ballot_w64(lane < xn && xk != 0ull);
+#pragma unroll
+            for (int r = 0; r < kMaxPeers; ++r)
+                if ((pend >> r) & 1u) bad |= __builtin_amdgcn_ballot_w64(needh && (uint32_t)(xh[r] >> 32) == atag);
+            if (bad != 0ull) { late = true; break; }
 #pragma unroll
             for (int r = 0; r < kMaxPeers; ++r) {
                 if (!((pend >> r) & 1u)) continue;
@@ -368,6 +386,24 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             if (pend == 0u) break;
             if (__builtin_amdgcn_s_memrealtime() - t_in > kPeerWaitTicks) { late = true; break; }   // (2 s)
             __builtin_amdgcn_s_sleep(1);
+        }
+        if (late && mode == 0) {
+            // Give the step up on every rank: this rank's timeout report into every rank's region
+            // (its own included), the step's abort tag over this block's header words in the peers'
+            // regions (a peer still polling this step gives it up too, instead of updating alone),
+            // and the sticky word the host reads (mppi_synchronize / mppi_read_outputs / mppi_peer_status).
+            const unsigned long long cw = ((unsigned long long)tag << 32) | 1ull;
+            const unsigned long long aw = (unsigned long long)atag << 32;
+#pragma unroll
+            for (int d = 0; d < kMaxPeers; ++d) {
+                if (d >= xn) continue;
+                gst64* rg = region(d);
+                if (lane == 0) __hip_atomic_store(rg - kXCtl + xme, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (d != xme && lane < kHdr)
+                    __hip_atomic_store(rg + off + lane, aw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            uint32_t* xe = T.xerr;   // (read only here: the late path)
+            if (lane == 0 && xe) __hip_atomic_store(xe, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         rho = INFINITY;
         nanf = late ? 2.0f : 0.0f;

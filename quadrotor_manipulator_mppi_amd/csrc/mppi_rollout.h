@@ -673,6 +673,9 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     const int sub = lane / LSEG, t0 = lane & (LSEG - 1);
     const int32_t noise_mode = noise_arg & 0xFF;
     const uint32_t step_ctr = step_of(step_arg, noise_arg);   // (native dispatch: from the dispatch id)
+    // the vehicle's Philox key: its index in the whole fleet (mppi_config.vehicle_offset rides in the
+    // noise argument's high half), so a fleet split over engines draws what one engine would
+    const uint32_t vkey = (uint32_t)v + ((uint32_t)noise_arg >> 16);
     STAMPRT(13);
     STAMP(0);
     // issue the global loads first (addresses need only preloaded scalars and the
@@ -718,7 +721,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         const uint32_t kg = k_off + (uint32_t)((blockIdx.x * nw + wid) * R + sub);
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
-            draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), (uint32_t)v, step_ctr, seed_lo, seed_hi);
+            draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), vkey, step_ctr, seed_lo, seed_hi);
     }
     STAMP(10);
     asm volatile("" :: "s"(kwarm));
@@ -809,7 +812,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
 #pragma unroll
                     for (int a = 0; a < NA; ++a) z[a] = z0[c][a];
                 } else {
-                    draw_normals<NA>(z, kg, (uint32_t)t, (uint32_t)v, step_ctr, seed_lo, seed_hi);
+                    draw_normals<NA>(z, kg, (uint32_t)t, vkey, step_ctr, seed_lo, seed_hi);
                 }
                 if (!XC || p.sigma_diag) {   // a full Sigma runs in the extended (XC) kernel
 #pragma unroll
@@ -1117,7 +1120,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
 #pragma unroll
         for (int s = 1; s < R; ++s) S_mine = (sub == s) ? S_seg[s] : S_mine;
         if (MPPI_S_PLAIN) { if (kval && t0 == 0) p.S[(size_t)v * K + k] = S_mine; }   // (experiment: round 3's plain store)
-        else if (kval && t0 == 0) s_stage[(it * nw + wid) * R + sub] = S_mine;
+        else if (kval && t0 == 0) s_stage[it * cost_run_stride(nw * R) + wid * R + sub] = S_mine;
 
         // ---- online softmin (mppi.py:184-188) over this wave's rollouts (scalar bookkeeping)
         float m = INFINITY;
@@ -1206,7 +1209,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         float* const Sv = uniform_ptr(p.S + (size_t)v * K);
         for (int i = lane; i < iters * q; i += 64) {
             const int it = i / q, k0 = (blockIdx.x + it * p.nb) * nS;
-            st_dev_run(Sv, (uint32_t)k0, s_stage + it * nS, min(nS, K - k0), i - it * q);
+            st_dev_run(Sv, (uint32_t)k0, s_stage + it * cost_run_stride(nS), min(nS, K - k0), i - it * q);
         }
     }
     // rho_b = the min of the 8 wave slots, which every thread reads for f_w anyway (an LDS
@@ -1278,9 +1281,10 @@ inline void rollout_symbol(char* buf, size_t n) {
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
 inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const int iters = ONEG ? 1 : p.iters;
-    // (LDS: warm start, 8 wave slots, the block's cost run of iters * 8 * R floats)
-    const int s_run = (iters * 8 * (64 / LSEG) + 3) & ~3;
-    if (threads <= 0 || threads > 512 || iters < 1 || iters * (threads / 64) * (64 / LSEG) > kMaxCostRun) return -1;
+    // (LDS: warm start, 8 wave slots, the block's cost runs: iters of them, one per group, each
+    // (threads / 64) * R floats padded to 16 B -- sized by the block's own waves, not by 8)
+    const int s_run = iters * cost_run_stride((threads / 64) * (64 / LSEG));
+    if (threads <= 0 || threads > 512 || iters < 1 || s_run > kMaxCostRun) return -1;
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>() + s_run) * sizeof(float);
     const int32_t geo = threads | (iters << 16);
     if (p.V == 1)

@@ -97,6 +97,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, v = blockIdx.y, b = blockIdx.x;
     const int32_t noise_mode = noise_arg & 0xFF;
     const uint32_t step_ctr = step_of(step_arg, noise_arg);   // (native dispatch: from the dispatch id)
+    const uint32_t vkey = (uint32_t)v + ((uint32_t)noise_arg >> 16);   // fleet-wide vehicle index (k_rollout)
     const int K = p.K;
     const int kb = b * QR;                       // the block's rollouts kb .. kb+QR-1
     float* const eps_t = qlds;
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(NT) k_rollout_quad(const uint32_t seed_lo, con
             eps[0] = n.x; eps[1] = n.y; eps[2] = n.z; eps[3] = n.w;
         } else {
             float z[kQA];
-            draw_normals<kQA>(z, k_off + (uint32_t)kc, (uint32_t)t, (uint32_t)v, step_ctr, seed_lo, seed_hi);
+            draw_normals<kQA>(z, k_off + (uint32_t)kc, (uint32_t)t, vkey, step_ctr, seed_lo, seed_hi);
             if (p.sigma_diag) {
 #pragma unroll
                 for (int a = 0; a < kQA; ++a) eps[a] = z[a] * p.sdiag[a];

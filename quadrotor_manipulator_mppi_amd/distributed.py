@@ -85,6 +85,15 @@ def _all_ranks_ok(ok: bool, group, device: int) -> bool:
     return bool(t.item())
 
 
+def _any_rank(flag: bool, group, device: int) -> bool:
+    """True if any rank passes flag (one MAX all-reduce; every rank returns the same verdict, and
+    every rank has joined it when it returns: it doubles as a barrier)."""
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                     device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
 def setup_native_comm(rank: int, world: int, group, device: int, available: Callable[[], Optional[str]],
                       make_id: Callable[[], bytes], init: Callable[[bytes], None]) -> Optional[str]:
     """Agree on, then build, the engine-owned RCCL communicator.  Returns None when every
@@ -163,9 +172,22 @@ def setup_peer_exchange(rank: int, world: int, group, device: int, engine: Engin
     return None
 
 
+def vehicle_range(n_vehicles: int, world: int, rank: int) -> range:
+    """The fleet-wide vehicles rank ``rank`` owns when a fleet of ``n_vehicles`` is split over
+    ``world`` GPUs ("prefer vehicles across GPUs -- zero communication"):
+    consecutive blocks of n_vehicles / world.  The engine is made with vehicle_offset = the range's
+    start, so its device noise is keyed by the fleet-wide index and each rank's vehicles draw, roll
+    out and finalise exactly as in one engine over the whole fleet."""
+    if n_vehicles % world:
+        raise ValueError(f"{n_vehicles} vehicles do not split over {world} ranks")
+    n = n_vehicles // world
+    return range(rank * n, (rank + 1) * n)
+
+
 def default_exchange(native: bool, world: int, n_vehicles: int) -> str:
     """MPPI_EXCHANGE (peer | rccl | torch; also over a gloo group, for rehearsals on one GPU) or,
-    for an engine-owned exchange, peer on one-vehicle shards of at most 8 ranks and RCCL otherwise."""
+    for an engine-owned exchange, peer on one-vehicle shards of at most 8 ranks and RCCL otherwise.
+    ("vehicles" -- the fleet split over the ranks, no exchange -- is chosen explicitly.)"""
     env = os.environ.get("MPPI_EXCHANGE")
     if env in ("peer", "rccl", "torch"):
         return env
@@ -175,7 +197,10 @@ def default_exchange(native: bool, world: int, n_vehicles: int) -> str:
 
 
 class ShardedEngine:
-    """One rank's engine of a sample-sharded MPPI controller."""
+    """One rank's engine of a sample-sharded MPPI controller -- or, with ``mode="vehicles"``, of a
+    vehicle-sharded fleet: ``n_vehicles`` is then the whole fleet, this rank's engine runs
+    ``vehicle_range(n_vehicles, world, rank)`` of it over all K samples, and nothing is exchanged
+    (each vehicle's softmin is its own; ``set_state`` / ``set_target`` take this rank's vehicles)."""
 
     def __init__(self, group=None, exchange: Callable = all_reduce_slots, native: Optional[bool] = None,
                  mode: Optional[str] = None, **engine_kw):
@@ -187,14 +212,20 @@ class ShardedEngine:
         self.native = bool(native)
         # the exchange: "peer" (no collective), "rccl" (engine-owned communicator), "torch"
         self.mode = mode or default_exchange(self.native, self.world, int(engine_kw.get("n_vehicles", 1) or 1))
-        if self.mode not in ("peer", "rccl", "torch"):
+        if self.mode not in ("peer", "rccl", "torch", "vehicles"):
             raise ValueError(f"exchange mode {self.mode!r}")
         self.native = self.mode != "torch"
         device = engine_kw.pop("device", 0)
         self.local = int(os.environ.get("LOCAL_RANK", device))
         self.local %= max(1, torch.cuda.device_count())   # more ranks than devices: wrap
         torch.cuda.set_device(self.local)
-        cfg = make_config(device=self.local, shard_rank=self.rank, shard_count=self.world, **engine_kw)
+        self.vehicles = range(int(engine_kw.get("n_vehicles", 1) or 1))   # the fleet-wide vehicles this rank runs
+        if self.mode == "vehicles":   # every rank a whole controller over its share of the fleet
+            self.vehicles = vehicle_range(len(self.vehicles), self.world, self.rank)
+            engine_kw = dict(engine_kw, n_vehicles=len(self.vehicles), vehicle_offset=self.vehicles.start)
+            cfg = make_config(device=self.local, shard_rank=0, shard_count=1, **engine_kw)
+        else:
+            cfg = make_config(device=self.local, shard_rank=self.rank, shard_count=self.world, **engine_kw)
         self.engine = Engine(cfg)
         # one dedicated stream carries rollout -> collective -> finalize (the default
         # stream's handle is 0, which mppi_set_stream reads as "engine-owned stream")
@@ -203,6 +234,7 @@ class ShardedEngine:
         self._exchange = exchange
         self.buf: Optional[torch.Tensor] = None
         self.native_error: Optional[str] = None
+        self.resyncs = 0   # peer-exchange recoveries (resync) so far
 
         def fresh_engine():
             self.engine.close()
@@ -228,7 +260,7 @@ class ShardedEngine:
                 fresh_engine()
             elif err is not None:
                 raise RuntimeError(err)
-        if not self.native and self.world > 1:
+        if not self.native and self.world > 1 and self.mode != "vehicles":
             slot = self.engine.exchange_slot_floats()
             with torch.cuda.stream(self.stream):
                 self.buf = torch.zeros(self.world * slot, dtype=torch.float32, device=f"cuda:{self.local}")
@@ -237,7 +269,7 @@ class ShardedEngine:
 
     def step_async(self, d_noise_ptr: int = 0):
         """rollout -> (all-reduce) -> finalize, all ordered on self.stream, no host sync."""
-        if self.native:
+        if self.native or self.mode == "vehicles":
             self.engine.rollout(d_noise_ptr)
             if self.mode == "rccl":
                 self.engine.exchange()
@@ -258,11 +290,76 @@ class ShardedEngine:
                 self.step_async()
 
     def step(self, state, d_noise_ptr: int = 0):
-        if (self.world == 1 or self.mode == "peer") and not d_noise_ptr:   # one C call, as the drop-in classes step
-            return self.engine.step(state)
-        self.engine.set_state(state)
-        self.step_async(d_noise_ptr)
-        return self.engine.read_outputs()
+        """One control step -> (out, u0, [StepStats]).  On a multi-rank peer exchange it is a
+        collective: the ranks agree on whether any of them gave the step up (one MAX all-reduce)
+        and, if so, resynchronise (``resync``) before returning, every rank reporting
+        ``exchange_timeout``."""
+        if (self.world == 1 or self.mode in ("peer", "vehicles")) and not d_noise_ptr:   # one C call, as the drop-in classes step
+            out, u0, st = self.engine.step(state)
+        else:
+            self.engine.set_state(state)
+            self.step_async(d_noise_ptr)
+            out, u0, st = self.engine.read_outputs()
+        if self._checks_exchange():
+            local = any(s.exchange_timeout for s in st)
+            if _any_rank(local, self.group, self.local):
+                self.resync()
+                for s in st:
+                    s.exchange_timeout = True
+                    s.nonfinite = True
+        return out, u0, st
+
+    # ------------------------------------------------------------- failure handling (peer)
+    def _checks_exchange(self) -> bool:
+        return self.mode == "peer" and self.world > 1
+
+    def synchronize(self) -> bool:
+        """Wait for this rank's steps.  On a multi-rank peer exchange it is a collective (and a
+        barrier): the ranks agree whether any of them gave a step up since the last check -- this
+        rank's sticky timeout word (any block of any step of a batch, mppi_synchronize's
+        MPPI_ERR_PEER_TIMEOUT) MAX-reduced over the process group -- and if one did, every rank
+        resynchronises (``resync``).  Returns True when it did (then every rank returns True)."""
+        from ._capi import PeerTimeout
+        local = False
+        try:
+            self.engine.synchronize()
+        except PeerTimeout:
+            local = True
+        if not self._checks_exchange():
+            if local:   # (one rank exchanging with itself cannot time out; a bad state all the same)
+                raise RuntimeError("peer exchange timeout on a one-rank exchange")
+            return False
+        if not _any_rank(local, self.group, self.local):
+            return False
+        self.resync()
+        return True
+
+    def resync(self):
+        """Collective recovery after a peer-exchange timeout (every rank calls it): every rank takes
+        rank 0's warm start u_prev and step counter and a fresh exchange epoch, and its exchange
+        region is cleared between two barriers (no kernel writes into any region while it is
+        cleared, and no rank steps before every region is clear).  Afterwards the ranks' warm starts
+        are bit-identical and the exchange runs again (the sharded reduction is
+        mppi.py:143-148)."""
+        from ._capi import PeerTimeout
+        eng = self.engine
+        try:
+            eng.synchronize()
+        except PeerTimeout:
+            pass
+        dev = f"cuda:{self.local}" if dist.get_backend(self.group) == "nccl" else "cpu"
+        u = torch.from_numpy(eng.get_u_prev()).to(dev)
+        _, _, epoch = eng.peer_status(reports=False)
+        ctl = torch.tensor([eng.get_step_counter(), epoch], dtype=torch.int64, device=dev)
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        dist.broadcast(u, src=src, group=self.group)
+        dist.broadcast(ctl, src=src, group=self.group)
+        step, epoch = (int(x) for x in ctl.tolist())
+        dist.barrier(group=self.group)
+        eng.peer_reset(step, epoch + 1)
+        dist.barrier(group=self.group)
+        eng.set_u_prev(u.cpu().numpy())
+        self.resyncs += 1
 
     def __getattr__(self, name):
         if name == "engine":

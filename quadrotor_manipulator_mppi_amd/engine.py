@@ -58,13 +58,14 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
                 state_f64: Optional[bool] = None, store_trajectory: bool = True, store_noise: bool = False,
                 check_reach: Optional[bool] = None, reach_tol: float = 0.005, blocks_per_vehicle: int = 0,
                 block_threads: int = 0, cost_terms=0, cost_weights: Optional[Dict[str, float]] = None,
-                quad: Optional[Dict] = None) -> capi.Config:
+                quad: Optional[Dict] = None, vehicle_offset: int = 0) -> capi.Config:
     """``cost_terms``: bitmask of ``capi.COST_*`` or an iterable of names among
     ``covar, center, joint_track, action, joint_limit`` -- the CostManager terms the
     reference ships disabled (cost_manager.py:83-87).  ``cost_weights`` overrides
     ``w_covar, cost_alpha, cost_gamma, w_center, w_joint_track, w_action,
     joint_limit_penalty``.  ``quad`` overrides the QUADROTOR rigid body: ``quad_mass``,
-    ``quad_inertia`` (3,), ``quad_kd``, ``quad_gravity``, ``quad_literal_jinv``."""
+    ``quad_inertia`` (3,), ``quad_kd``, ``quad_gravity``, ``quad_literal_jinv``.  ``vehicle_offset``:
+    the fleet-wide index of vehicle 0 (vehicle sharding: the device noise is keyed by it)."""
     L = capi.lib()
     cfg = capi.Config()
     L.mppi_config_default(C.byref(cfg), MODELS[model])
@@ -106,6 +107,7 @@ def make_config(model: str = "arm", n_samples: Optional[int] = None, n_horizon: 
     cfg.seed = seed
     cfg.device = device
     cfg.shard_rank, cfg.shard_count = shard_rank, shard_count
+    cfg.vehicle_offset = vehicle_offset
     if state_f64 is not None:
         cfg.state_f64 = int(state_f64)
     cfg.store_trajectory = int(store_trajectory)
@@ -241,6 +243,26 @@ class Engine:
     def peer_probe(self, phase: int):
         """Connection check (collective): phase 0 on every rank, a barrier, then phase 1."""
         capi.check(self._L.mppi_peer_probe(self._h, int(phase)), "peer_probe")
+
+    def peer_status(self, reports: bool = True):
+        """(sticky, reports, epoch) of the peer exchange (mppi_peer_status): ``sticky`` = this
+        engine's timeout word (the given-up step's tag, 0 = none; host memory), ``reports`` = the
+        timeout reports in this rank's region (one per rank, 0 = none; a device read, None when
+        ``reports`` is False), ``epoch`` = the exchange epoch of the tags."""
+        st, ep = C.c_uint32(0), C.c_uint32(0)
+        rep = (C.c_uint64 * capi.MAX_PEERS)() if reports else None
+        capi.check(self._L.mppi_peer_status(self._h, C.byref(st), rep, C.byref(ep)), "peer_status")
+        return st.value, (list(rep) if reports else None), ep.value
+
+    def peer_reset(self, step: int, epoch: int):
+        """Clear this rank's region and sticky word, take the agreed step counter and epoch
+        (collective recovery: every rank synchronised, a barrier before and after)."""
+        capi.check(self._L.mppi_peer_reset(self._h, step & 0xFFFFFFFF, epoch & 0xFFFFFFFF), "peer_reset")
+
+    def get_step_counter(self) -> int:
+        x = C.c_uint32(0)
+        capi.check(self._L.mppi_get_step_counter(self._h, C.byref(x)), "get_step_counter")
+        return x.value
 
     def set_stream(self, stream_handle: int):
         capi.check(self._L.mppi_set_stream(self._h, C.c_void_p(stream_handle)), "set_stream")

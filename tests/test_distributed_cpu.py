@@ -328,3 +328,165 @@ def test_default_exchange(monkeypatch):
     assert default_exchange(True, 8, 1) == "rccl"
     monkeypatch.setenv("MPPI_EXCHANGE", "peer")
     assert default_exchange(False, 2, 1) == "peer"
+
+
+# ---------------------------------------------------------------- vehicle sharding (config C5)
+class _TargetSink:
+    """Stands in for an Engine where bench.set_targets writes the per-vehicle targets."""
+    def __init__(self):
+        self.t = {}
+
+    def set_target(self, pos, quat=None, vehicle=0):
+        self.t[vehicle] = (np.asarray(pos, np.float32), np.asarray(quat, np.float32))
+
+
+def _fleet_oracle_steps(vehicles, V_total, K=48, H=16, seed=77, steps=2):
+    """The control steps of the fleet-wide vehicles ``vehicles`` as one rank of a vehicle split
+    computes them: its rows of the fleet's state (bench.make_state), its targets (bench.set_targets
+    with the rank's range), and the device noise keyed by the FLEET-WIDE vehicle index
+    (O.philox_normals, the kernel's draw restated) -- through the oracle's whole-body step."""
+    import bench
+    from quadrotor_manipulator_mppi_amd.robot.urdf_chain import load_chain
+    torch.set_num_threads(1)
+    chain = [O.Joint(j["name"], j["type"], j["xyz"], j["rpy"], j["axis"], j["q_index"]) for j in load_chain()]
+    state = bench.make_state("wholebody", vehicles.stop)[vehicles.start:]
+    sink = _TargetSink()
+    bench.set_targets(sink, "wholebody", vehicles)
+    sig = np.diag([30.0] * 3 + [0.1] * 7).astype(np.float32)
+    out = {}
+    for i, v in enumerate(vehicles):
+        s = state[i]
+        tpos, tquat = sink.t[i]
+        u = torch.zeros(H, 10)
+        rpy = O.base_rpy_from_quat(s[3:7])
+        res = []
+        for step in range(steps):
+            _, z = O.philox_normals(seed, step, v, np.arange(K), H, 10)
+            noise = torch.from_numpy(z) @ torch.from_numpy(sig)
+            r = O.wholebody_step(chain, s[0:3], s[14:17], s[7:14], s[17:24], rpy, u, noise, tpos, tquat)
+            u = r["u_prev_out"]
+            res.append((r["S"].numpy(), u.numpy(), r["qdes"].numpy()))
+        out[v] = res
+    return out
+
+
+def _vehicle_split_main(rank, world, port, V, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd.distributed import vehicle_range
+        vr = vehicle_range(V, world, rank)
+        mine = _fleet_oracle_steps(vr, V)
+        got = [None] * world
+        dist.all_gather_object(got, (rank, list(vr), mine))   # (no collective on the step path: results only)
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_vehicle_split_equals_one_fleet():
+    """Config C5 split over 2 ranks by vehicles (ShardedEngine mode "vehicles", SURVEY §8e "prefer
+    vehicles across GPUs -- zero communication"): each rank takes vehicle_range(8, 2, rank), its rows
+    of the fleet's state and its targets from bench.py, and the noise keyed by the fleet-wide vehicle
+    index; every rank's vehicles equal one process over the whole fleet bit for bit (the GPU side of
+    the same claim: tests/test_gpu_fleet.py test_vehicle_split_*)."""
+    from quadrotor_manipulator_mppi_amd.distributed import vehicle_range
+    V, world = 8, 2
+    assert [list(vehicle_range(V, world, r)) for r in range(world)] == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    with pytest.raises(ValueError):
+        vehicle_range(7, 2, 0)
+    whole = _fleet_oracle_steps(range(V), V)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vehicle_split_main, args=(r, world, port, V, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got in res:
+        owned = sorted(v for _, vs, _ in got for v in vs)
+        assert owned == list(range(V)), "every vehicle owned by exactly one rank"
+        for _, vs, mine in got:
+            for v in vs:
+                for (S, u, qd), (S1, u1, qd1) in zip(mine[v], whole[v]):
+                    assert np.array_equal(S, S1) and np.array_equal(u, u1) and np.array_equal(qd, qd1), v
+
+
+# ---------------------------------------------------------------- peer-exchange timeout agreement
+class _FakeTimeoutEngine:
+    """The engine calls ShardedEngine.synchronize / resync make, on the host only (no GPU here):
+    rank ``late`` reports a timeout (mppi_synchronize's MPPI_ERR_PEER_TIMEOUT) until reset."""
+    def __init__(self, rank, late):
+        from quadrotor_manipulator_mppi_amd import _capi
+        self._exc = _capi.PeerTimeout
+        self.timed_out = rank == late
+        self.u = np.full((1, 4, 3), float(rank + 1), np.float32)
+        self.ctr, self.epoch = 10 + rank, 3 + rank
+        self.resets = []
+
+    def synchronize(self):
+        if self.timed_out:
+            raise self._exc(-6, "peer exchange: a step was given up")
+
+    def get_u_prev(self):
+        return self.u.copy()
+
+    def set_u_prev(self, u):
+        self.u = np.asarray(u, np.float32).copy()
+
+    def get_step_counter(self):
+        return self.ctr
+
+    def peer_status(self, reports=True):
+        return (1 if self.timed_out else 0), None, self.epoch
+
+    def peer_reset(self, step, epoch):
+        self.timed_out = False
+        self.ctr, self.epoch = step, epoch
+        self.resets.append((step, epoch))
+
+
+def _agree_main(rank, world, port, late, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
+        se = object.__new__(ShardedEngine)   # (the host protocol only: no Engine, no HIP stream)
+        se.group, se.rank, se.world, se.local, se.mode, se.resyncs = None, rank, world, 0, "peer", 0
+        se.engine = _FakeTimeoutEngine(rank, late)
+        first = se.synchronize()
+        second = se.synchronize()
+        e = se.engine
+        q.put((rank, first, second, e.u, e.ctr, e.epoch, e.resets, se.resyncs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("late", [0, 1, None])
+def test_gloo_world2_peer_timeout_agreement_and_resync(late):
+    """ShardedEngine.synchronize on a multi-rank peer exchange (the host side of the failure
+    handling; the device side is tests/test_gpu_peer.py): the ranks MAX-agree on any rank's
+    timeout, so EVERY rank reports it (True) even when only one rank's engine saw it, and every
+    rank resynchronises -- rank 0's warm start and step counter, epoch + 1, its region reset -- so
+    the warm starts are identical afterwards; no timeout: nothing happens on any rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_main, args=(r, world, port, late, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if late is None:
+        assert all(r[1] is False and r[2] is False and r[6] == [] for r in res)
+        return
+    for rank, first, second, u, ctr, epoch, resets, n in res:
+        assert first is True and second is False and n == 1, (rank, first, second, n)
+        assert np.array_equal(u, np.full((1, 4, 3), 1.0, np.float32)), "rank 0's warm start on every rank"
+        assert (ctr, epoch) == (10, 4) and resets == [(10, 4)]

@@ -407,3 +407,113 @@ def test_arm_generic_chain_extended_kernel(kinova_path_off, monkeypatch):
     raw, sm = e.get_weighted_noise()
     _check_reduction(S, raw[0], sm[0], e.get_u_prev()[0], r, noise.numpy(), 9, "arm generic chain")
     e.close()
+
+
+# ------------------------------------------------------------------ vehicle sharding (C5 over GPUs)
+def _fleet_state(V):
+    """Fleet-wide states and targets as bench.py makes them (row / target v = vehicle v)."""
+    import bench
+    return bench.make_state("wholebody", V)
+
+
+def _fleet_engine(V, K, H, offset=0, **kw):
+    e = _engine(model="wholebody", n_samples=K, n_horizon=H, n_vehicles=V, seed=77, vehicle_offset=offset,
+                blocks_per_vehicle=32, **kw)
+    return e
+
+
+def _set_fleet_targets(e, vehicles):
+    import bench
+    bench.set_targets(e, "wholebody", vehicles)
+
+
+@pytest.mark.parametrize("dispatch", ["aql", "hip"])
+def test_vehicle_split_equals_one_fleet_engine(dispatch, monkeypatch):
+    """SURVEY §8e for C5 -- the fleet's vehicles split over engines with nothing exchanged
+    (ShardedEngine mode "vehicles"): two engines over vehicles [0, 4) and [4, 8) (vehicle_offset 0
+    and 4: the device noise is keyed by the fleet-wide vehicle index) equal ONE engine over all 8
+    vehicles bit for bit -- costs, warm starts after a native batch, and control-call outputs --
+    at the same per-vehicle geometry (blocks_per_vehicle pinned; the auto geometry depends on V)."""
+    monkeypatch.setenv("MPPI_DISPATCH", dispatch)
+    V, K, H = 8, 1024, 64
+    full = _fleet_engine(V, K, H)
+    halves = [_fleet_engine(4, K, H, offset=o) for o in (0, 4)]
+    state = _fleet_state(V)
+    _set_fleet_targets(full, range(V))
+    full.set_state(state)
+    for i, e in enumerate(halves):
+        _set_fleet_targets(e, range(4 * i, 4 * i + 4))
+        e.set_state(state[4 * i:4 * i + 4])
+    try:
+        for e in [full] + halves:
+            e.run_steps(12)
+            e.synchronize()
+        assert np.array_equal(np.concatenate([e.get_u_prev() for e in halves]), full.get_u_prev())
+        assert np.array_equal(np.concatenate([e.get_costs() for e in halves]), full.get_costs())
+        st2 = state.copy()
+        st2[:, 7:14] += 0.01
+        o_f, u_f, s_f = full.step(st2)
+        parts = [e.step(st2[4 * i:4 * i + 4]) for i, e in enumerate(halves)]
+        assert np.array_equal(np.concatenate([p[0] for p in parts]), o_f)
+        assert np.array_equal(np.concatenate([p[1] for p in parts]), u_f)
+        assert [(s.rho, s.eta) for p in parts for s in p[2]] == [(s.rho, s.eta) for s in s_f]
+    finally:
+        for e in [full] + halves:
+            e.close()
+
+
+def _vehicle_rank(rank, world, port, V, K, H, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
+        se = ShardedEngine(mode="vehicles", model="wholebody", n_samples=K, n_horizon=H, n_vehicles=V, seed=77,
+                           blocks_per_vehicle=32)
+        _set_fleet_targets(se.engine, se.vehicles)
+        se.engine.set_state(_fleet_state(V)[se.vehicles.start:se.vehicles.stop])
+        se.run_steps(10)
+        assert se.synchronize() is False
+        out, u0, st = se.step(_fleet_state(V)[se.vehicles.start:se.vehicles.stop])
+        q.put((rank, se.mode, se.vehicles.start, se.engine.V, se.engine.get_u_prev(), out, se.engine.dispatch_info()))
+        se.engine.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_vehicle_split_two_processes_equal_one_engine():
+    """The same through ShardedEngine(mode="vehicles") in two processes (gloo group, one GPU): each
+    rank's engine runs its half of the fleet; nothing is exchanged; the ranks' warm starts and
+    outputs, concatenated, equal one engine over the whole fleet bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    V, K, H = 8, 1024, 64
+    full = _fleet_engine(V, K, H)
+    _set_fleet_targets(full, range(V))
+    full.set_state(_fleet_state(V))
+    full.run_steps(10)
+    full.synchronize()
+    o_f, _, _ = full.step(_fleet_state(V))
+    u_f = full.get_u_prev()
+    full.close()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_vehicle_rank, args=(r, 2, port, V, K, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert [(r[1], r[2], r[3]) for r in res] == [("vehicles", 0, 4), ("vehicles", 4, 4)]
+    assert all(r[6].startswith("aql;") for r in res), [r[6] for r in res]
+    assert np.array_equal(np.concatenate([r[4] for r in res]), u_f)
+    assert np.array_equal(np.concatenate([r[5] for r in res]), o_f)

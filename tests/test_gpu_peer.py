@@ -236,17 +236,20 @@ def _timeout_rank(rank, world, port, q):
     try:
         from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
         se = ShardedEngine(mode="peer", model="wholebody", n_samples=1024, n_horizon=H, seed=SEED)
+        se.engine.set_target(*TARGET)
+        u_in = (np.arange(H * 10, dtype=np.float32).reshape(1, H, 10) % 7 - 3.0) * 0.01
         res = None
         if rank == 0:   # rank 1 never steps: this rank's finalize gives up after its 2 s bound
-            se.engine.set_target(*TARGET)
-            u_in = (np.arange(H * 10, dtype=np.float32).reshape(1, H, 10) % 7 - 3.0) * 0.01
             se.engine.set_u_prev(u_in)
             t0 = time.perf_counter()
-            out, u0, st = se.step(STATE)
+            out, u0, st = se.engine.step(STATE)   # (the engine alone: no agreement with rank 1)
             res = (time.perf_counter() - t0, (st[0].nonfinite, st[0].exchange_timeout), bool(np.isfinite(out).all()),
                    bool(np.array_equal(se.engine.get_u_prev(), u_in)), float(u0[0, 0]), float(u_in[0, 0, 0]))
-        dist.barrier()
-        q.put((rank, se.mode, res))
+        # both ranks: the agreement (ShardedEngine.synchronize) sees rank 0's timeout and resynchronises
+        resynced = se.synchronize()
+        u_after = se.engine.get_u_prev()
+        sticky, reports, _ = se.engine.peer_status()
+        q.put((rank, se.mode, res, resynced, u_after, sticky, reports, se.engine.get_step_counter()))
         se.engine.close()
     finally:
         dist.destroy_process_group()
@@ -255,7 +258,9 @@ def _timeout_rank(rank, world, port, q):
 def test_peer_timeout_keeps_warm_start():
     """A rank whose peer never steps: its finalize blocks wait out the 2 s bound, then the step
     keeps the warm start (u_prev unchanged, outputs from it, finite) and reports nonfinite = 2
-    (StepStats.nonfinite and .exchange_timeout)."""
+    (StepStats.nonfinite and .exchange_timeout).  Then both ranks' ShardedEngine.synchronize agree
+    on the timeout and resynchronise: rank 1 (which never stepped) ends with rank 0's warm start
+    and step counter, and both exchanges are reset (no sticky word, no reports)."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -277,6 +282,140 @@ def test_peer_timeout_keeps_warm_start():
     assert nonfinite == (True, True) and finite and kept, res[0][2]
     assert u0 == u_in0, "u0 is the kept warm start's first step"
     assert 1.5 < dt < 30.0, dt
+    assert res[0][3] and res[1][3], "every rank reports the timeout (ShardedEngine.synchronize)"
+    assert np.array_equal(res[0][4], res[1][4]), "after the resync the ranks' warm starts are bit-identical"
+    assert res[0][7] == res[1][7], "and their step counters"
+    assert all(r[5] == 0 and not any(r[6]) for r in res), "the exchanges are reset"
+
+
+def _pair(G=2, k=512, **kw):
+    """G in-process peer ranks (mppi_peer_connect_ptrs) on this GPU, whole-body K = k each."""
+    ranks = [_engine(n_samples=k, shard_rank=r, shard_count=G, **kw) for r in range(G)]
+    for e in ranks:
+        e.peer_open()
+    addrs = [e.peer_region() for e in ranks]
+    for e in ranks:
+        e.peer_connect_ptrs(addrs)
+        e.set_state(STATE)
+    return ranks
+
+
+def _sync_all(ranks):
+    """Synchronise every engine; True per engine whose mppi_synchronize reported a timeout."""
+    from quadrotor_manipulator_mppi_amd import _capi
+    out = []
+    for e in ranks:
+        try:
+            e.synchronize()
+            out.append(False)
+        except _capi.PeerTimeout:
+            out.append(True)
+    return out
+
+
+def _resync_in_process(ranks):
+    """ShardedEngine.resync for ranks in one process (no process group): rank 0's warm start, step
+    counter and epoch + 1 on every rank, every region cleared with every engine idle."""
+    _sync_all(ranks)
+    u = ranks[0].get_u_prev()
+    step = ranks[0].get_step_counter()
+    epoch = ranks[0].peer_status(reports=False)[2]
+    for e in ranks:
+        e.peer_reset(step, epoch + 1)
+    for e in ranks:
+        e.set_u_prev(u)
+
+
+def test_peer_timeout_rank_wide_and_resync():
+    """Two in-process ranks; rank 1 runs ONE STEP FEWER in a native batch, so rank 0's last step
+    times out.  After the batch every rank reports it -- rank 0 through its sticky word and
+    mppi_synchronize's MPPI_ERR_PEER_TIMEOUT, rank 1 through the timeout report rank 0's blocks
+    stored into rank 1's region (mppi_peer_status) -- and while the exchange stays unreset every
+    further step on every rank is given up at once (no 2 s waits, warm starts held, reported by
+    every block of every step).  After the in-process resync the ranks' u_prev are bit-identical,
+    and further native batches stay bit-identical with no timeout."""
+    import time
+    ranks = _pair()
+    try:
+        for e in ranks:
+            e.run_steps(3)
+        assert _sync_all(ranks) == [False, False]
+        n = 6
+        ranks[0].run_steps(n)
+        ranks[1].run_steps(n - 1)
+        t0 = time.perf_counter()
+        timed = _sync_all(ranks)
+        dt = time.perf_counter() - t0
+        assert timed[0] and 1.5 < dt < 30.0, (timed, dt)
+        st0, rep0, _ = ranks[0].peer_status()
+        st1, rep1, _ = ranks[1].peer_status()
+        assert st0 != 0 and rep0[0] != 0, (st0, rep0)
+        assert rep1[0] != 0, f"rank 1's region holds rank 0's timeout report: {rep1}"
+        reported = [st != 0 or any(rep) for st, rep in ((st0, rep0), (st1, rep1))]
+        assert reported == [True, True], "every rank reports the timeout after the batch"
+        _, _, stats0 = ranks[0].read_outputs()
+        assert stats0[0].exchange_timeout and stats0[0].nonfinite
+        # broken until reset: both ranks give every step up at once and hold their warm starts
+        held = [e.get_u_prev() for e in ranks]
+        t0 = time.perf_counter()
+        for e in ranks:
+            e.run_steps(4)
+        timed = _sync_all(ranks)
+        dt = time.perf_counter() - t0
+        assert timed == [True, True] and dt < 1.0, (timed, dt)
+        assert all(np.array_equal(e.get_u_prev(), u) for e, u in zip(ranks, held)), "warm starts held"
+        _resync_in_process(ranks)
+        assert np.array_equal(ranks[0].get_u_prev(), ranks[1].get_u_prev())
+        assert [e.peer_status()[0] for e in ranks] == [0, 0]
+        for e in ranks:
+            e.run_steps(8)
+        assert _sync_all(ranks) == [False, False]
+        u = [e.get_u_prev() for e in ranks]
+        assert np.array_equal(u[0], u[1]) and np.isfinite(u[0]).all(), "ranks bit-identical after the resync"
+        assert not np.array_equal(u[0], held[0]), "and stepping again"
+        for e in ranks:
+            _, _, st = e.read_outputs()
+            assert not st[0].exchange_timeout
+    finally:
+        for e in ranks:
+            e.close()
+
+
+def test_peer_replay_in_lockstep_takes_no_stale_words():
+    """both ranks rewind the step counter (mppi_set_step_counter) and replay a step from
+    another warm start.  The replayed step's parity slots still hold the first run's words of the
+    same step counter; the exchange epoch in the tags (moved by set_step_counter) keeps a rank that
+    polls before its peer has rewritten them from taking them.  Rank 1's replay is enqueued 50 ms
+    after rank 0's, so rank 0 polls while only stale words are there.  Result: bit-identical to a
+    fresh pair run from the same warm start and counter."""
+    import time
+    rep_pair, fresh = _pair(), _pair()
+    try:
+        for e in rep_pair:
+            e.run_steps(4)
+        _sync_all(rep_pair)
+        ctr = rep_pair[0].get_step_counter()
+        for e in rep_pair:
+            e.run_steps(2)
+        assert _sync_all(rep_pair) == [False, False]
+        u_alt = (rep_pair[0].get_u_prev() + np.float32(0.05)).astype(np.float32)   # another warm start
+        for pair in (rep_pair, fresh):
+            for e in pair:
+                e.set_u_prev(u_alt)
+                e.set_step_counter(ctr)
+        for e in fresh:
+            e.run_steps(2)
+        rep_pair[0].run_steps(2)
+        time.sleep(0.05)
+        rep_pair[1].run_steps(2)
+        assert _sync_all(fresh) == [False, False] and _sync_all(rep_pair) == [False, False]
+        want = fresh[0].get_u_prev()
+        assert np.array_equal(fresh[1].get_u_prev(), want)
+        for r, e in enumerate(rep_pair):
+            assert np.array_equal(e.get_u_prev(), want), f"rank {r}: the replay took stale partials"
+    finally:
+        for e in rep_pair + fresh:
+            e.close()
 
 
 def test_peer_probe_failure_falls_back_on_every_rank():
