@@ -367,11 +367,9 @@ static unsigned char* batch_args(Step* s) { return s->d_args + (1 + 2 * (size_t)
 
 int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
                  uint32_t step_off, std::string* err) {
-    // the next rollout's packet index: a batch of (rollout, finalize) pairs counts steps by
-    // (index >> 1); a batch of fused steps (fin.symbol empty: one packet per step) by the index
-    const bool single = fin.symbol[0] == '\0';
-    const uint64_t wi = hsa_queue_load_write_index_relaxed(s->q);
-    const uint32_t word = step - (uint32_t)(single ? wi : (wi >> 1));
+    // the next rollout's packet index (the queue holds (rollout, finalize) pairs only, so
+    // rollouts sit at indices of one parity and (index >> 1) counts pairs)
+    const uint32_t word = step - (uint32_t)(hsa_queue_load_write_index_relaxed(s->q) >> 1);
     if (s->valid && s->step_word == word && s->step_off == step_off && same_launch(roll, s->roll, step_off) &&
         same_launch(fin, s->fin, ~0u))
         return 0;
@@ -385,19 +383,19 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
         fprintf(stderr, "[mppi aql] re-upload: word %u vs %u, rollout args differ at %d, finalize at %d, sym %d/%d\n", word,
                 s->step_word, first, ffirst, strcmp(roll.symbol, s->roll.symbol), strcmp(fin.symbol, s->fin.symbol));
     }
-    Kern kr, kf{};
+    Kern kr, kf;
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        if (!lookup(s->dev, roll.symbol, &kr, err) || (!single && !lookup(s->dev, fin.symbol, &kf, err))) return -2;
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
     }
-    if (!check_launch(roll, kr, err) || (!single && !check_launch(fin, kf, err))) return -2;
+    if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
     if (step_off + 4 > roll.arg_bytes) { *err = "step counter outside the rollout's arguments"; return -2; }
     // the queue may still be reading the blocks about to be overwritten
     if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
     std::vector<unsigned char> h(2 * kArgSlot, 0);
     memcpy(h.data(), roll.args, roll.arg_bytes);
     memcpy(h.data() + step_off, &word, 4);
-    if (!single) memcpy(h.data() + kArgSlot, fin.args, fin.arg_bytes);
+    memcpy(h.data() + kArgSlot, fin.args, fin.arg_bytes);
     // a fresh pair of blocks for every upload (no cached copy of an earlier upload can be read)
     s->batch_slot = (s->batch_slot + 1) % kBatchSlots;
     if (hipMemcpy(batch_args(s), h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -544,16 +542,10 @@ int step_dispatch(Step* s, int n, std::string* err) {
     void* ra = batch_args(s);
     void* fa = batch_args(s) + kArgSlot;
     load_fences();
-    const bool single = s->fin.symbol[0] == '\0';   // fused steps: the rollout packet is the whole step
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
-        if (single) {
-            put(s->q, s->kr, s->roll, ra, last ? s->done : none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0],
-                last ? 2 : g_fence[3]);
-        } else {
-            put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
-            put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
-        }
+        put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
+        put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
         // the doorbell takes the index of the last packet written
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     }
@@ -568,19 +560,18 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     static long pcn = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
     const auto p0 = now();
-    const bool single = fin.symbol[0] == '\0';   // a fused step: one packet
-    Kern kr, kf{};
+    Kern kr, kf;
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        if (!lookup(s->dev, roll.symbol, &kr, err) || (!single && !lookup(s->dev, fin.symbol, &kf, err))) return -2;
+        if (!lookup(s->dev, roll.symbol, &kr, err) || !lookup(s->dev, fin.symbol, &kf, err)) return -2;
     }
-    if (!check_launch(roll, kr, err) || (!single && !check_launch(fin, kf, err))) return -2;
+    if (!check_launch(roll, kr, err) || !check_launch(fin, kf, err)) return -2;
     if (step_off + 4 > roll.arg_bytes || seq_off + 4 > roll.arg_bytes) { *err = "call words outside the arguments"; return -2; }
     // the host block is rewritten below: the previous call's rollout must have read it.  The
     // engine reads every call's outputs before the next call (its flag: that rollout has run),
     // so only an unread call waits; a queued batch does not read this block.
     if (s->call_unread && s->outstanding && step_wait(s, 60000, err) != 0) return -1;
-    if (!single && (!s->call_valid || !same_launch(fin, s->fin_call, ~0u))) {
+    if (!s->call_valid || !same_launch(fin, s->fin_call, ~0u)) {
         if (s->outstanding && step_wait(s, 60000, err) != 0) return -1;
         std::vector<unsigned char> h(kArgSlot, 0);
         memcpy(h.data(), fin.args, fin.arg_bytes);
@@ -595,8 +586,8 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     s->kc_r = kr;
     s->kc_f = kf;
     const uint64_t r = hsa_queue_load_write_index_relaxed(s->q);   // this call's rollout packet
-    const uint32_t word = step - (uint32_t)(single ? r : (r >> 1));
-    *seq = 0x80000000u | (uint32_t)r;   // (the packet index: unique and increasing whatever the step's packet count)
+    const uint32_t word = step - (uint32_t)(r >> 1);
+    *seq = 0x80000000u | (uint32_t)(r >> 1);
     const uint32_t slot = s->call_slot++ % kCallSlots;
     unsigned char* blk = s->h_call + (size_t)slot * kArgSlot;
     alignas(16) unsigned char tmp[kArgSlot];
@@ -624,12 +615,8 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     s->call_unread = true;
     const hsa_signal_t none{0};
     load_fences();
-    if (single) {
-        put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, s->done, std::max(1, g_fence[0]), 2);
-    } else {
-        put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
-        put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
-    }
+    put(s->q, kr, roll, s->h_call_dev + (size_t)slot * kArgSlot, none, std::max(1, g_fence[0]), g_fence[1]);
+    put(s->q, kf, fin, s->d_args, s->done, g_fence[2], 2);
     hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
     if (prof) {
         const auto p4 = now();
@@ -645,20 +632,6 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
 }
 
 int step_error(Step* s) { return s ? s->qerr.load() : 0; }
-
-int step_nop(Step* s) {
-    if (!s) return -1;
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(s->q, 1);
-    while (idx - hsa_queue_load_read_index_scacquire(s->q) >= s->q->size) _mm_pause();
-    auto* p = (hsa_barrier_and_packet_t*)s->q->base_address + (idx & (s->q->size - 1));
-    memset((char*)p + 4, 0, sizeof(*p) - 4);
-    const uint16_t header = (uint16_t)((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                                       (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                       (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-    __atomic_store_n((uint32_t*)p, (uint32_t)header, __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)idx);
-    return 0;
-}
 
 const char* step_call_memory(Step* s) {
     return !s ? "" : s->call_vis ? s->dev->vis_pool_kind.c_str() : "pinned host memory";

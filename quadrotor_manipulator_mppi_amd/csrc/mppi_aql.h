@@ -55,9 +55,6 @@ void step_call_read(Step* s);
 const char* step_call_memory(Step* s);
 // The queue's asynchronous error, if any (0 = none).
 int step_error(Step* s);
-// diagnostics (tools/probes.py rate): one no-op barrier-AND packet on the engine's queue, no
-// completion signal -- does a queue that stays busy keep a control call's latency low?
-int step_nop(Step* s);
 // Until every dispatched pair has completed.  -1 on a queue error or after timeout_ms.
 int step_wait(Step* s, int timeout_ms, std::string* err);
 bool step_busy(Step* s);

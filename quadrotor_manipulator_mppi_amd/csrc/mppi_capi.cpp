@@ -374,11 +374,6 @@ struct mppi_engine {
     float* d_gamma = nullptr;     //   gamma^t (H)
     float* d_jtraj = nullptr;     //   joint tracking target (V,H,nq)
     float* d_exchange = nullptr;
-    // the fused step (k_rollout finalises the step: one launch per step, mppi_rollout.h fused_tail):
-    // possible for this engine's kernels (fuse_ok), taken while the engine exchanges nothing (fused())
-    bool fuse_ok = false;
-    uint32_t* d_tickets = nullptr;      // (V, kTicketStride) arrival counters
-    float* d_grec = nullptr;            // (V, G, P) group records
     ncclComm_t comm = nullptr;          // engine-owned RCCL communicator (mppi_comm_init)
     float* d_xown = nullptr;            // its exchange buffer (shard_count * V * P floats)
     bool peer = false;                  // peer exchange connected (mppi_peer_connect): no PACK, no collective
@@ -426,11 +421,6 @@ namespace {
 // communicator (a one-rank communicator runs the same pack -> all-reduce -> combine).  A shard
 // connected by the peer exchange steps like an unsharded engine: its finalize does the exchange.
 bool sharded(const mppi_engine* e) { return (e->cfg.shard_count > 1 || e->comm) && !e->peer; }
-
-// The engine's steps are fused (one k_rollout launch that finalises the step, mppi_rollout.h
-// fused_tail) when its kernels allow it and it exchanges nothing (sharded and peer-exchange steps
-// combine the ranks' partials in k_finalize).  MPPI_FUSED=0 keeps the two-kernel step.
-bool fused(const mppi_engine* e) { return e->fuse_ok && !sharded(e) && !e->peer && !e->d_stamps; }
 
 FinTail tail_of(const FinParams& f, int32_t mode) {
     FinTail t;
@@ -871,11 +861,6 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     }
     if (nb > 4096) { delete e; return fail(MPPI_ERR_INVALID_ARG, "too many rollout blocks (%d)", nb); }
     const int P = (kHdr + e->A * H + 3) & ~3;
-    // The fused step's block groups (mppi_rollout.h fused_tail): G a power of two with G^2 >= nb (two
-    // folds of ~sqrt(nb) records each), at most kMaxGroups groups of at most 64 blocks, G <= nb.
-    int fuse_g = 1, fuse_lg = 0;
-    while (fuse_g * fuse_g < nb || (nb + fuse_g - 1) / fuse_g > 64) { fuse_g *= 2; ++fuse_lg; }
-    while (fuse_g > nb) { fuse_g /= 2; --fuse_lg; }
     // the rollout kernels address one vehicle's trajectory planes through a buffer
     // resource (32-bit byte offsets) and the record bodies with 32-bit indices
     if (c.store_trajectory && (uint64_t)e->C * ((e->K + 15) & ~15) * ((H + 15) & ~15) * sizeof(float) > 0xFFFFFFFFull) {
@@ -919,20 +904,6 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     CREATE_TRY(hipMalloc(&e->d_w, sizeof(float) * e->V * e->K));
     CREATE_TRY(hipMalloc(&e->d_hdr, sizeof(float) * (size_t)e->V * nb * 4));
     CREATE_TRY(hipMalloc(&e->d_rdata, sizeof(float) * (size_t)e->V * e->A * nb * H));
-    {   // the fused step: the common kernel at NCH == 1 (mppi_rollout.h launch_rollout_x), not the quadrotor
-        bool diag = true;
-        for (int a = 0; a < e->A; ++a)
-            for (int b = 0; b < e->A; ++b) diag = diag && (a == b || c.sigma[a * e->A + b] == 0.0f);
-        const char* fz = getenv("MPPI_FUSED");
-        e->fuse_ok = !(fz && !strcmp(fz, "0")) && c.model != MPPI_MODEL_QUADROTOR && nch == 1 && !c.cost_terms && diag &&
-                     fuse_g <= kMaxGroups && (nb + fuse_g - 1) / fuse_g <= 64;
-        // (the chain condition -- the Kinova fast path -- is checked below once the chain is baked)
-    }
-    if (e->fuse_ok) {
-        CREATE_TRY(hipMalloc(&e->d_tickets, sizeof(uint32_t) * (size_t)e->V * kTicketStride));
-        CREATE_TRY(hipMemset(e->d_tickets, 0, sizeof(uint32_t) * (size_t)e->V * kTicketStride));
-        CREATE_TRY(hipMalloc(&e->d_grec, sizeof(float) * (size_t)e->V * fuse_g * P));
-    }
     CREATE_TRY(hipMalloc(&e->d_wraw, sizeof(float) * e->V * H * e->A));
     CREATE_TRY(hipMalloc(&e->d_wsmooth, sizeof(float) * e->V * H * e->A));
     if (c.store_trajectory) CREATE_TRY(hipMalloc(&e->d_traj, sizeof(float) * traj_floats(e)));
@@ -1046,9 +1017,6 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     for (int d = 0; d < 3; ++d) p.q_iinv[d] = (float)(1.0 / (double)c.quad_inertia[d]);
     p.q_kd = c.quad_kd; p.q_g = c.quad_gravity; p.q_literal_jinv = c.quad_literal_jinv ? 1 : 0;
     p.vc = e->d_vc; p.u_prev = e->d_u_prev;
-    p.tickets = e->d_tickets; p.grec = e->d_grec; p.fuse_g = fuse_g; p.fuse_lg = fuse_lg;
-    p.ftail = nullptr;   // (set per launch: fused_params)
-    if (c.model != MPPI_MODEL_DRONE && p.chain_fast != 2) e->fuse_ok = false;   // (a generic chain: the XC kernel)
     p.traj = e->d_traj; p.noise_out = e->d_noise_out; p.S = e->d_S; p.hdr = e->d_hdr; p.rdata = e->d_rdata;
 #ifdef MPPI_STAMPS
     if (getenv("MPPI_STAMPS")) {
@@ -1139,7 +1107,7 @@ void mppi_destroy(mppi_engine* e) {
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->comm) rccl().destroy(e->comm);
     for (void* q : e->x_opened) if (q) (void)hipIpcCloseMemHandle(q);
-    void* dev[] = {e->d_tickets, e->d_grec, e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
+    void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
                    e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
     for (void* p : dev) if (p) (void)hipFree(p);
@@ -1623,42 +1591,6 @@ mppi_status mppi_finalize(mppi_engine* e) {
     return finalize_impl(e, true);
 }
 
-// One fused step through HIP (fused(e)): k_rollout with the FINAL tail, so the step is one launch;
-// the bookkeeping of finalize_impl (the read step's sequence number, its output event, the step
-// counter).  The split phases (mppi_rollout / mppi_finalize) stay two kernels.
-static mppi_status launch_fused(mppi_engine* e, const float* d_noise, bool record_out) {
-    if (use_device(e)) return MPPI_ERR_HIP;
-    DevParams p = e->dp;
-    p.noise_in = d_noise;
-    p.vc0 = e->h_vc[0];
-    p.step_ctr = e->step_ctr;
-    p.ftail = (e->out_dbg == 1 && !record_out) ? e->d_tail + kTailScratch : e->d_tail + kTailFinal;
-    p.fin_seq = 0u;
-    if (record_out && !e->no_flag_dbg) {   // as finalize_impl: a fresh value per read step, never 0
-        p.fin_seq = ++e->seq_ctr & 0x7FFFFFFFu;
-        if (p.fin_seq == 0u) p.fin_seq = ++e->seq_ctr & 0x7FFFFFFFu;
-    }
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (e->timing) { e0 = pool_event(e); e1 = pool_event(e); HIP_TRY(hipEventRecord(e0, e->stream)); }
-    const int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-    if (rc != 0) return fail(MPPI_ERR_HIP, "fused step launch failed (%d: %s)", rc,
-                             rc > 0 ? hipGetErrorString((hipError_t)rc) : "no kernel for this model/A/H");
-    if (e->timing) {
-        HIP_TRY(hipEventRecord(e1, e->stream));
-        e->roll_pairs.emplace_back(e0, e1);
-        if (e->roll_pairs.size() >= 2048) { mppi_status st = drain_timing(e); if (st) return st; }
-    }
-    if (record_out) {
-        e->out_seq = p.fin_seq;
-        HIP_TRY(hipEventRecord(e->ev_out, e->stream));   // outputs land in mapped host memory
-    }
-    ++e->step_ctr;
-    e->out_pending = record_out;
-    e->aql_out = false;
-    e->aql_call = false;
-    return MPPI_OK;
-}
-
 // True when every output record of the pending read step carries its sequence number (the
 // tag is each record's last word; k_finalize writes a record with one 16 B store).
 static bool records_tagged(const mppi_engine* e, uint32_t want) {
@@ -1876,11 +1808,6 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         HIP_TRY(hipMemcpyAsync(e->d_noise_in, h_noise, n * sizeof(float), hipMemcpyHostToDevice, e->stream));
         dn = e->d_noise_in;
     }
-    if (fused(e)) {
-        if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_step before mppi_set_state");
-        if ((st = launch_fused(e, dn, true)) != MPPI_OK) return st;
-        return mppi_read_outputs(e, out, u0, stats);
-    }
     if ((st = mppi_rollout(e, dn)) != MPPI_OK) return st;
     if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
     if ((st = mppi_finalize(e)) != MPPI_OK) return st;
@@ -1904,7 +1831,6 @@ static const char* aql_ineligible(const mppi_engine* e, bool batch = false) {
 // native dispatch it is relative to the dispatch id (kNoiseStepFromId in the noise-mode word).
 constexpr uint32_t kRollStepOff = 8;
 constexpr int32_t kNoiseStepFromId = 0x100;   // = mppi_device.h
-constexpr int32_t kNoiseStepFromId1 = 0x200;  // = mppi_device.h: one packet per (fused) step
 
 // n steps as native AQL packets (mppi_aql.cpp).  *used = false: the caller runs them through
 // HIP (auto mode, native dispatch unavailable for this engine; e->aql_why says why).
@@ -1942,13 +1868,11 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     const auto c1 = now();
     LaunchDesc& roll = e->batch_roll;
     LaunchDesc& fin = e->batch_fin;
-    const bool fz = fused(e);   // one packet per step (k_rollout finalises it) or a (rollout, finalize) pair
     DevParams p = e->dp;
     p.noise_in = nullptr;
     p.vc0 = e->h_vc[0];
     p.step_ctr = 0u;                      // (set by step_prepare: relative to the dispatch id)
-    p.noise_mode |= fz ? kNoiseStepFromId1 : kNoiseStepFromId;
-    if (fz) { p.ftail = e->d_tail + kTailFinal; p.fin_seq = 0u; }   // (completion: the batch's signal)
+    p.noise_mode |= kNoiseStepFromId;
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // completion: the batch's signal, not a flag
@@ -1958,11 +1882,10 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
         e->batch_cached = false;
         mppi_aql::set_capture(&roll);
         int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0 && !fz) {
+        if (rc == 0) {
             mppi_aql::set_capture(&fin);
             rc = mppi_launch_finalize(&f, e->stream);
         }
-        if (fz) fin.symbol[0] = '\0';   // (no second packet)
         mppi_aql::set_capture(nullptr);
         if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
         e->batch_p = p;
@@ -2027,13 +1950,11 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
         else if (q != hipSuccess) return fail(MPPI_ERR_HIP, "engine stream: %s", hipGetErrorString(q));
     }
     const auto q3 = std::chrono::steady_clock::now();
-    const bool fz = fused(e);
     DevParams p = e->dp;
     p.noise_in = nullptr;
     p.vc0 = e->h_vc[0];
     p.step_ctr = 0u;
-    p.noise_mode |= fz ? kNoiseStepFromId1 : kNoiseStepFromId;
-    if (fz) { p.ftail = e->d_tail + kTailFinal; p.fin_seq = kSeqFromVc; }   // (the call's number: vc._pad[0])
+    p.noise_mode |= kNoiseStepFromId;
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = kSeqFromVc;
@@ -2056,11 +1977,10 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
         e->call_cached = false;
         mppi_aql::set_capture(&roll);
         int rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0 && !fz) {
+        if (rc == 0) {
             mppi_aql::set_capture(&fin);
             rc = mppi_launch_finalize(&f, e->stream);
         }
-        if (fz) fin.symbol[0] = '\0';   // (no second packet)
         mppi_aql::set_capture(nullptr);
         if (rc != 0) return fail(MPPI_ERR_HIP, "describing the step's launches failed (%d)", rc);
         e->call_p = p;
@@ -2106,12 +2026,7 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     bool used = false;
     mppi_status st = run_steps_aql(e, n, &used);
     if (st != MPPI_OK || used) return st;
-    const bool fz = fused(e);
     for (int i = 0; i < n; ++i) {
-        if (fz) {
-            if ((st = launch_fused(e, nullptr, i == n - 1)) != MPPI_OK) return st;
-            continue;
-        }
         mppi_status st = mppi_rollout(e, nullptr);
         if (st != MPPI_OK) return st;
         if (e->comm && (st = mppi_exchange(e)) != MPPI_OK) return st;
@@ -2159,21 +2074,19 @@ mppi_status mppi_kernel_timing_ex(mppi_engine* e, int32_t n, double* rollout_us,
         hipError_t _e = (expr);                                                             \
         if (_e != hipSuccess) { st = fail(MPPI_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e)); goto done; } \
     } while (0)
-    const bool fz = fused(e);   // a fused engine: its step is ONE launch (rollout_us = pair_us, finalize_us = 0)
-    if (fz) { p.ftail = f.tail; p.fin_seq = 0u; }
     KT_TRY(hipMalloc(&saved, ub));
     for (auto& x : ev) KT_TRY(hipEventCreate(&x));
     KT_TRY(hipMemcpyAsync(saved, e->d_u_prev, ub, hipMemcpyDeviceToDevice, e->stream));
     KT_TRY(hipEventRecord(ev[0], e->stream));
     for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_rollout(&p, e->threads, e->stream);
     KT_TRY(hipEventRecord(ev[1], e->stream));
-    for (int i = 0; i < n && rc == 0 && !fz; ++i) rc = mppi_launch_finalize(&f, e->stream);
+    for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_finalize(&f, e->stream);
     KT_TRY(hipEventRecord(ev[2], e->stream));
     // the kernels as a control step runs them: rollout after finalize (u_prev and the
     // records just written, cold in the other XCDs' L2)
     for (int i = 0; i < n && rc == 0 && pair_us; ++i) {
         rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0 && !fz) rc = mppi_launch_finalize(&f, e->stream);
+        if (rc == 0) rc = mppi_launch_finalize(&f, e->stream);
     }
     KT_TRY(hipEventRecord(ev[3], e->stream));
     KT_TRY(hipMemcpyAsync(e->d_u_prev, saved, ub, hipMemcpyDeviceToDevice, e->stream));
@@ -2230,52 +2143,6 @@ extern "C" mppi_status mppi_probe_sequence(mppi_engine* e, int32_t n, int32_t mo
 }
 #endif
 
-// diagnostics (tools/probes.py fused; not in the header): n fused steps back to back (outputs into
-// device scratch) and n two-kernel (rollout, finalize) pairs, event-timed on the engine stream;
-// u_prev restored afterwards
-extern "C" mppi_status mppi_debug_fused_timing(mppi_engine* e, int32_t n, double* fused_us, double* pair_us) {
-    if (!e || n <= 0 || !fused_us || !pair_us) return fail(MPPI_ERR_INVALID_ARG, "bad arguments");
-    if (!e->fuse_ok) return fail(MPPI_ERR_STATE, "this engine's kernels have no fused step");
-    if (!e->state_set) return fail(MPPI_ERR_STATE, "before mppi_set_state");
-    if (use_device(e)) return MPPI_ERR_HIP;
-    const size_t ub = sizeof(float) * e->V * e->H * e->A;
-    float* saved = nullptr;
-    hipEvent_t ev[3];
-    HIP_TRY(hipMalloc(&saved, ub));
-    for (auto& x : ev) HIP_TRY(hipEventCreate(&x));
-    DevParams p = e->dp;
-    p.vc0 = e->h_vc[0];
-    p.step_ctr = e->step_ctr;
-    DevParams pf = p;
-    pf.ftail = e->d_tail + kTailScratch;
-    pf.fin_seq = 0u;
-    FinParams f = e->fp;
-    f.mode = 0; f.seq = 0u;
-    final_records(e, f);
-    f.tail = e->d_tail + kTailScratch;
-    HIP_TRY(hipMemcpyAsync(saved, e->d_u_prev, ub, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipEventRecord(ev[0], e->stream));
-    int rc = 0;
-    for (int i = 0; i < n && rc == 0; ++i) rc = mppi_launch_rollout(&pf, e->threads, e->stream);
-    HIP_TRY(hipEventRecord(ev[1], e->stream));
-    for (int i = 0; i < n && rc == 0; ++i) {
-        rc = mppi_launch_rollout(&p, e->threads, e->stream);
-        if (rc == 0) rc = mppi_launch_finalize(&f, e->stream);
-    }
-    HIP_TRY(hipEventRecord(ev[2], e->stream));
-    HIP_TRY(hipMemcpyAsync(e->d_u_prev, saved, ub, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    float ms0 = 0.0f, ms1 = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms0, ev[0], ev[1]));
-    HIP_TRY(hipEventElapsedTime(&ms1, ev[1], ev[2]));
-    for (auto x : ev) (void)hipEventDestroy(x);
-    (void)hipFree(saved);
-    if (rc != 0) return fail(MPPI_ERR_HIP, "launch failed (%d)", rc);
-    *fused_us = 1e3 * ms0 / n;
-    *pair_us = 1e3 * ms1 / n;
-    return MPPI_OK;
-}
-
 mppi_status mppi_kernel_timing(mppi_engine* e, int32_t n, double* rollout_us, double* finalize_us) {
     return mppi_kernel_timing_ex(e, n, rollout_us, finalize_us, nullptr);
 }
@@ -2303,17 +2170,11 @@ mppi_status mppi_exchange_timing(mppi_engine* e, int32_t n, double* allreduce_us
     return st;
 }
 
-// diagnostics (tools/probes.py rate; not in the header): one no-op packet on the engine's native queue
-extern "C" mppi_status mppi_debug_queue_nop(mppi_engine* e) {
-    if (!e || !e->aql) return fail(MPPI_ERR_STATE, "no native queue");
-    return mppi_aql::step_nop(e->aql) == 0 ? MPPI_OK : fail(MPPI_ERR_HIP, "nop packet");
-}
-
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len) {
     if (!e || !buf || len <= 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_dispatch_info: bad arguments");
-    snprintf(buf, (size_t)len, "%s%s; calls: %s%s%s; step: %s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str(),
+    snprintf(buf, (size_t)len, "%s%s; calls: %s%s%s", e->aql_why.empty() ? "aql" : "hip: ", e->aql_why.c_str(),
              e->calls_native ? "aql (arguments in " : "hip", e->calls_native ? mppi_aql::step_call_memory(e->aql) : "",
-             e->calls_native ? ")" : "", fused(e) ? "fused (one launch)" : "rollout + finalize");
+             e->calls_native ? ")" : "");
     return MPPI_OK;
 }
 

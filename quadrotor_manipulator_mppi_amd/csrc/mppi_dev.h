@@ -70,15 +70,6 @@ constexpr KinOrigin kKinova[7] = {
     {{0, 2, 1}, {-1, -1, -1}, 2},   // joint_7: rpy (-pi/2, 0, pi),   xyz (0, .10375, 0)
 };
 
-struct FinTail;
-
-// The fused step (k_rollout finalises the step itself; mppi_capi.cpp fused()): arrival counters,
-// one per block group and one per vehicle, each on a 128 B line of its own (arrivals on different
-// counters then do not serialise on one line); the vehicle counter after the (<= kMaxGroups) group ones
-constexpr int kMaxGroups = 64;
-constexpr int kTicketPitch = 32;                              // uint32 words between counters
-constexpr int kTicketStride = (kMaxGroups + 1) * kTicketPitch;  // words per vehicle
-
 struct DevParams {
     int32_t model, V, K, H, A;
     int32_t L;          // lanes per rollout segment (pow2 >= H, <= 64)
@@ -134,12 +125,6 @@ struct DevParams {
     float q_g;                    // gravity magnitude, g = (0, 0, -q_g)
     int32_t q_literal_jinv;       // t >= 1 applies inv(J) to the body rates, as the commented loop
                                   // (drone_mppi.py:73-76); 0 = J at every step
-    // the fused step (k_rollout fused_tail): null ftail = the two-kernel step (k_finalize follows)
-    const FinTail* ftail;         // the FINAL tail parameters: outputs, SavGol taps, dt
-    uint32_t* tickets;            // (V, kTicketStride) arrival counters, zero between steps
-    float* grec;                  // (V, G, P) group records: (rho, eta, eta2, nan) + N[a][t]
-    int32_t fuse_g, fuse_lg;      // block groups per vehicle G (a power of two <= kMaxGroups), log2 G
-    uint32_t fin_seq;             // the read step's sequence number (0: none; kSeqFromVc: vc._pad[0])
 };
 constexpr int kStamps = 16;
 

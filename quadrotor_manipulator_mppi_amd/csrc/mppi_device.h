@@ -25,11 +25,8 @@ namespace {
 // relative to the dispatch id -- step = arg + (dispatch id >> 1) -- so one argument block,
 // written once, serves every (rollout, finalize) pair the engine's queue runs
 constexpr int32_t kNoiseStepFromId = 0x100;
-// ... and for a queue of fused steps (one packet per step: k_rollout finalises): step = arg + id
-constexpr int32_t kNoiseStepFromId1 = 0x200;
 __device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg) {
-    return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1)
-           : (noise_arg & kNoiseStepFromId1) ? step_arg + (uint32_t)mppi_dispatch_id() : step_arg;
+    return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
 }
 
 // Loads of what one kernel of a step hands the next (record bodies and headers, u_prev, the

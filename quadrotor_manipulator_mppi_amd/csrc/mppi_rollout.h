@@ -637,206 +637,6 @@ __device__ __forceinline__ void integrate_lds(const float (&act)[NA], float* xw,
     for (int a2 = 0; a2 < NA; ++a2) inc[a2] = xw[lane * P + a2];
 }
 
-// =============================================================================
-// The fused step's tail (DevParams::ftail set; mppi_capi.cpp fused()): the block records of
-// the step are folded and the step finalised inside k_rollout, with no second launch.
-//   1. Arrival: the blocks of a vehicle form G groups (block b in group b mod G, G a power of
-//      two); every block, once each of its waves has drained its write-through record stores,
-//      adds one to its group's counter, and the block whose add comes LAST folds the group's
-//      ng = nb / G records (MI355X_MICROARCH.md hand-off table, row 1: one lane per storing
-//      workgroup adds to one unsharded counter, the last adder loads with sc1 loads after its add
-//      returned, its other waves after a workgroup barrier).  G counters of ~nb / G arrivals each
-//      instead of one of nb: the round-4 fused negative lost 3.2-3.5 us to the fan-in
-//      of 256 tickets on ONE counter, and its folding blocks each re-read all 256 records.
-//   2. Group fold: rho_g = min rho_r, f_r = exp(-(rho_r - rho_g)/lambda), eta_g = sum f_r eta_r,
-//      eta2_g = sum f_r^2 eta2_r, N_g = sum f_r N_r (records in increasing index), written
-//      through as the group's record; then one add on the vehicle's counter.
-//   3. Final (the vehicle's last group): the G group records folded the same way, then the
-//      finalize's FINAL math element by element (mppi.py:144-158, svg_filter.py:13-90):
-//      w_eps = N / eta, the SavGol correlation with the symmetric pad, u += w_eps (no shift), and
-//      the outputs of t = 0 into mapped host memory (qdes with the OLD u_prev[0], mppi.py:157),
-//      the stats and the tagged output records, exactly as k_finalize writes them.
-// The last adder of each counter resets it, so every counter is zero again when the launch ends.
-// =============================================================================
-#ifndef MPPI_FOLD_BATCH
-#define MPPI_FOLD_BATCH 8
-#endif
-constexpr int kFoldBatch = MPPI_FOLD_BATCH;   // record loads in flight per thread in the fused tail's folds
-template <int MODEL, int NA, bool F64>
-__device__ __forceinline__ void fused_tail(const DevParams& p, const int v, const int tid, const int nthr,
-                                           const int H, float* scratch, const float* u_lds,
-                                           const VehicleConst& vc) {
-    constexpr int QOFF = (MODEL == MPPI_MODEL_WHOLEBODY) ? 3 : 0;
-    const int lane = tid & 63;
-    const int HA = H * NA;
-    const int G = p.fuse_g, nb = p.nb;
-    const int g = blockIdx.x & (G - 1);
-    const int ng = (nb - g + G - 1) >> p.fuse_lg;                     // this group's blocks (<= 64)
-    uint32_t* const tk = p.tickets + (size_t)v * kTicketStride;
-    uint32_t* const flag = (uint32_t*)scratch;                        // LDS: the block's verdict
-    float* const fsh = scratch + 4;                                    // LDS: f_r per record (<= 64)
-    float* const wl = scratch + 4 + 64;                                // LDS: w_eps of the final, (a, t)
-    const float coef = p.coef;
-    const float rH = __builtin_amdgcn_rcpf((float)H);   // (a, t) of element e = a H + t: a = trunc((e + 1/2) / H)
-    auto last_arrival = [&](uint32_t* ctr, uint32_t n) {   // (every wave's stores drained before)
-        lds_barrier();
-        if (tid == 0) {
-            const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t last = (old == n - 1u) ? 1u : 0u;
-            if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next step
-            flag[0] = last;
-        }
-        lds_barrier();
-        return __builtin_amdgcn_readfirstlane(flag[0]) != 0u;
-    };
-    // Fold n <= 64 records: header r at hdr + r hs (4 floats), element e of record r at
-    // body + off(e) + r bs.  Every wave reads the n headers (lane r) and folds them alike, so
-    // (rho, eta, eta2, nan) are the same in every wave; each element's sum runs over r in
-    // increasing order.  Device-scope (sc1) loads: written through by other CUs and drained
-    // before their adds.  use(e, N_e) per element.
-    float rho, eta, eta2, nanf;
-    auto fold = [&](const float* hdr, uint32_t hs, const float* body, uint32_t bs, int n, auto&& off, auto&& use) {
-        float hx = INFINITY, hy = 0.0f, hz = 0.0f, hw = 0.0f;
-        if (lane < n) {
-            const float* hp = hdr + (size_t)lane * hs;
-            hx = ld_dev(hp); hy = ld_dev(hp + 1); hz = ld_dev(hp + 2); hw = ld_dev(hp + 3);
-        }
-        rho = wave_fold_all(hx, OpMin());
-        const float f = (hx < INFINITY) ? __expf(coef * (hx - rho)) : 0.0f;
-        eta = wave_fold_all(f * hy, OpAdd());
-        eta2 = wave_fold_all((f * f) * hz, OpAdd());
-        nanf = wave_fold_all(hw, OpMax());
-        if (tid < 64) fsh[lane] = f;
-        lds_barrier();
-        // body loads through one buffer resource over the (uniform) base: a 32-bit byte offset per
-        // load, no 64-bit address math (the ONEG kernels' tail must fit their 64-VGPR budget)
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(body), 0, (int)0x7FFFFFFF, 0x00020000);
-        const uint32_t sb = bs * 4u;
-        for (int e = tid; e < HA; e += nthr) {
-            const uint32_t ob = (uint32_t)off(e) * 4u;
-            float acc = 0.0f;
-            for (int r0 = 0; r0 < n; r0 += kFoldBatch) {   // a batch of records' loads in flight, then their sum
-                float x[kFoldBatch];
-#pragma unroll
-                for (int i = 0; i < kFoldBatch; ++i)
-                    x[i] = (r0 + i < n) ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(ob + (uint32_t)(r0 + i) * sb), 0, kAuxDev))
-                                        : 0.0f;
-#pragma unroll
-                for (int i = 0; i < kFoldBatch; ++i) acc = fmaf((r0 + i < n) ? fsh[r0 + i] : 0.0f, x[i], acc);
-            }
-            use(e, acc);
-        }
-    };
-    // ---- 1. group arrival (every wave has drained its record stores)
-    drain_stores();
-    if (!last_arrival(tk + g * kTicketPitch, (uint32_t)ng)) return;
-#ifdef MPPI_FUSED_KO   // timing knockouts (results wrong): 1 = arrival only, 2 = + group fold, 3 = + vehicle arrival
-    if (MPPI_FUSED_KO == 1) return;
-#endif
-    // ---- 2. group fold: the records of blocks b = g + j G (j < ng), header at hdr[v][b], element
-    //         (a, t) at rdata[v][a][b][t]; the group's record goes to grec[v][g] (header, N[a H + t])
-    const int P = p.P;
-    float* const grec_v = p.grec + (size_t)v * G * P;
-    {
-        float* const gdst = uniform_ptr(grec_v + (size_t)g * P);
-        const uint32_t nbh = (uint32_t)nb * (uint32_t)H;
-        fold(p.hdr + ((size_t)v * nb + g) * 4, (uint32_t)G * 4u, p.rdata + (size_t)v * NA * nbh + (size_t)g * H,
-             (uint32_t)G * (uint32_t)H, ng,
-             [&](int e) {
-                 const int a = (int)(((float)e + 0.5f) * rH), t = e - a * H;
-                 return (size_t)a * nbh + (size_t)t;
-             },
-             [&](int e, float N) { wt_store(gdst, (uint32_t)(kHdr + e) * 4u, N); });
-        if (tid == 0) wt_store4(gdst, 0u, make_float4(rho, eta, eta2, nanf));
-    }
-    drain_stores();
-#ifdef MPPI_FUSED_KO
-    if (MPPI_FUSED_KO == 2) return;
-#endif
-    if (!last_arrival(tk + kMaxGroups * kTicketPitch, (uint32_t)G)) return;
-#ifdef MPPI_FUSED_KO
-    if (MPPI_FUSED_KO == 3) return;
-#endif
-    // ---- 3. final (the vehicle's last group): fold the G group records, then w_eps, SavGol,
-    //         u += w_eps and the outputs (k_finalize's FINAL, element by element)
-    fold(grec_v, (uint32_t)P, grec_v + kHdr, (uint32_t)P, G, [&](int e) { return (size_t)e; },
-         [&](int e, float N) { wl[e] = N; });
-    const FinTail& T = *p.ftail;
-    const int window = T.window, hf = window >> 1;
-    const float etaf = (nanf > 0.0f) ? NAN : eta;
-    lds_barrier();
-    for (int e = tid; e < HA; e += nthr) wl[e] = __fdividef(wl[e], etaf);
-    lds_barrier();
-    float* const up = uniform_ptr(const_cast<float*>(p.u_prev) + (size_t)v * HA);   // (V, H, A): (t, a) at t A + a
-    // the outputs' pointers and the step's sequence number (scalar loads, uniform)
-    double* const outp = T.out + (size_t)v * T.out_dim;
-    float* const u0p = T.u0 + (size_t)v * NA;
-    float* const stats = T.stats + (size_t)v * 4;
-    uint32_t* const flags = T.flags;
-    const int odim = T.out_dim;
-    const float dt = p.dt, dt2 = p.dt2;
-    uint32_t seqv = p.fin_seq;
-    if (seqv == kSeqFromVc) seqv = __float_as_uint(vc._pad[0]);
-    const float ess = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
-    for (int e = tid; e < HA; e += nthr) {
-        const int a = (int)(((float)e + 0.5f) * rH), t = e - a * H;
-        const float* wa = wl + a * H;
-        // SavGol with the reference's symmetric pad (svg_filter.py:58): index -i-1 left of 0,
-        // 2H-1-i right of H-1; the taps flipped for the correlation (FinTail::sg, as k_finalize)
-        float sm = 0.0f;
-        for (int j = 0; j < window; ++j) {
-            int q = t - hf + j;
-            q = (q < 0) ? -q - 1 : (q >= H) ? 2 * H - 1 - q : q;
-            sm = fmaf(T.sg[j], wa[q], sm);
-        }
-        const float u_old = u_lds[t * NA + a];
-        const float un = u_old + sm;
-        __hip_atomic_store(up + t * NA + a, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (written through)
-        if (t == 0) {   // this dim's outputs (mppi.py:157-158, drone_mppi.py:168-169), as k_finalize
-#pragma clang fp contract(off)
-            const float u0 = un;
-            u0p[a] = u0;
-            double o1 = 0.0, o2 = 0.0;
-            const bool drone_dim = (MODEL == MPPI_MODEL_DRONE) || (MODEL == MPPI_MODEL_WHOLEBODY && a < 3);
-            if (drone_dim) {
-                const float x0 = vc.pos0f[a], v0 = vc.vel0f[a];
-                const float xo = (x0 + v0 * dt) + (0.5f * u0) * dt2;
-                const float vo = v0 + dt * u0;
-                o1 = xo;
-                o2 = vo;
-                outp[a] = o1;
-                outp[3 + a] = o2;
-            } else {
-                const int nq = NA - QOFF, j = a - QOFF;
-                const int base = (MODEL == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
-                const float t1 = u_old * dt;
-                const float t2 = ((0.5f * u0) * dt) * dt;
-                const float t3 = u0 * dt;
-                if (F64 && MODEL == MPPI_MODEL_ARM) {
-                    o1 = (vc.pos0[a] + (double)t1) + (double)t2;
-                    o2 = vc.vel0[a] + (double)t3;
-                } else {
-                    o1 = (double)((vc.pos0f[a] + t1) + t2);
-                    o2 = (double)(vc.vel0f[a] + t3);
-                }
-                outp[base + j] = o1;
-                outp[base + nq + j] = o2;
-            }
-            if (a == 0) { stats[0] = rho; stats[1] = eta; stats[2] = ess; stats[3] = nanf; }
-            if (seqv != 0u) {   // tagged output records (k_finalize "Completion"): one 16 B store each
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                u32x4* rec = reinterpret_cast<u32x4*>(flags) + (size_t)v * (2 * NA + 1);
-                const uint64_t b1 = (uint64_t)__double_as_longlong(o1), b2 = (uint64_t)__double_as_longlong(o2);
-                rec[2 * a] = u32x4{(uint32_t)b1, (uint32_t)(b1 >> 32), __float_as_uint(u0), seqv};
-                rec[2 * a + 1] = u32x4{(uint32_t)b2, (uint32_t)(b2 >> 32), __float_as_uint(nanf), seqv};
-                if (a == 0) rec[2 * NA] = u32x4{__float_as_uint(rho), __float_as_uint(eta), __float_as_uint(ess), seqv};
-            }
-        }
-    }
-    drain_stores();
-}
-
 // The leading scalar arguments are preloaded into SGPRs at wave launch on gfx950
 // (-mllvm -amdgpu-kernarg-preload-count, build.py): the first group's Philox
 // draw and the u_prev / joint-table loads start without waiting for the
@@ -847,7 +647,7 @@ __device__ __forceinline__ void fused_tail(const DevParams& p, const int v, cons
 // arm kernel would spill at 64 and keeps the 4-wave budget -- C3 runs 2 waves per SIMD).  At the C4 shard
 // (whole-body K=8192 H=64) that is 1024 blocks x 8 waves, all resident at once: twice the
 // latency hiding of 512 blocks x 2 groups, and no wave left alone in the grid's tail.
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG, bool FU>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
 __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH == 2 ? (XC ? MPPI_ROLL_OCC_NCH2_XC : MPPI_ROLL_OCC_NCH2) : (XC ? MPPI_ROLL_OCC_XC : MPPI_ROLL_OCC))) k_rollout(const uint32_t seed_lo, const uint32_t seed_hi,
                                                  const uint32_t step_arg, const uint32_t k_off,
                                                  const int32_t noise_arg, const int32_t H_arg,
@@ -1466,22 +1266,19 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     STAMP(7);
     STAMPRT(14);
     drain_stores();
-    // the fused step (FU: its own instantiations, so the two-kernel step's registers are untouched):
-    // the last-arriving blocks fold the records and finalise the step (fused_tail)
-    if constexpr (FU) fused_tail<MODEL, NA, F64>(p, v, tid, nthr, H, wsh, u_lds, vc);
 }
 
 // =============================================================================
 // launchers
 // =============================================================================
 // the instantiation's symbol (native dispatch looks it up in the code object)
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG, bool FU>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool VONE, bool XC, bool ONEG>
 inline void rollout_symbol(char* buf, size_t n) {
-    snprintf(buf, n, "_Z9k_rolloutILi%dELi%dELi%dELi%dELb%dELb%dELb%dELb%dELb%dEEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE",
-             MODEL, NA, NCH, LSEG, (int)F64, (int)VONE, (int)XC, (int)ONEG, (int)FU);
+    snprintf(buf, n, "_Z9k_rolloutILi%dELi%dELi%dELi%dELb%dELb%dELb%dELb%dEEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE",
+             MODEL, NA, NCH, LSEG, (int)F64, (int)VONE, (int)XC, (int)ONEG);
 }
 
-template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG, bool FU>
+template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC, bool ONEG>
 inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const int iters = ONEG ? 1 : p.iters;
     // (LDS: warm start, 8 wave slots, the block's cost runs: iters of them, one per group, each
@@ -1491,31 +1288,22 @@ inline int launch_rollout_g(const DevParams& p, int threads, hipStream_t s) {
     const size_t lds = (size_t)(((p.H * NA + 3) & ~3) + 8 * wave_slot_floats<NA, NCH, LSEG>() + s_run) * sizeof(float);
     const int32_t geo = threads | (iters << 16);
     if (p.V == 1)
-        return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG, FU>,
-                  rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG, FU>, dim3(p.nb, p.V), dim3(threads), lds, s,
+        return go(k_rollout<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>,
+                  rollout_symbol<MODEL, NA, NCH, LSEG, F64, true, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
                   p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev,
                   p.joints, p);
-    return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG, FU>,
-              rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG, FU>, dim3(p.nb, p.V), dim3(threads), lds, s,
+    return go(k_rollout<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>,
+              rollout_symbol<MODEL, NA, NCH, LSEG, F64, false, XC, ONEG>, dim3(p.nb, p.V), dim3(threads), lds, s,
               p.seed_lo, p.seed_hi, p.step_ctr, (uint32_t)p.k_offset, p.noise_mode, p.H, geo, p.u_prev, p.joints,
               p);
 }
 
 // the single-group (ONEG) variant exists for the common kernel at NCH == 1
-// The fused step (DevParams::ftail set, mppi_capi.cpp fused()) is instantiated for the common kernel
-// at NCH == 1 only (H <= 64: the latency-bound shapes whose finalize launch it removes); the host
-// asks for it nowhere else.
 template <int MODEL, int NA, int NCH, int LSEG, bool F64, bool XC>
 inline int launch_rollout_x(const DevParams& p, int threads, hipStream_t s) {
-    if constexpr (!XC && NCH == 1) {
-        if (p.ftail) {
-            if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true, true>(p, threads, s);
-            return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false, true>(p, threads, s);
-        }
-        if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true, false>(p, threads, s);
-    }
-    if (p.ftail) return -1;
-    return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false, false>(p, threads, s);
+    if constexpr (!XC && NCH == 1)
+        if (p.iters == 1) return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, true>(p, threads, s);
+    return launch_rollout_g<MODEL, NA, NCH, LSEG, F64, XC, false>(p, threads, s);
 }
 
 // The extended (XC) instantiation carries the extra CostManager terms, a full

@@ -31,21 +31,18 @@ def test_every_kernel_unit_has_a_gfx950_code_object():
         assert flags & 0xFF == 0x4F, f"{path}: not gfx950 (mach {flags & 0xFF:#x})"
 
 
-def _rollout(model, na, nch, lseg, f64, vone, xc, oneg, fu=False):
+def _rollout(model, na, nch, lseg, f64, vone, xc, oneg):
     return (f"_Z9k_rolloutILi{model}ELi{na}ELi{nch}ELi{lseg}ELb{int(f64)}ELb{int(vone)}ELb{int(xc)}ELb{int(oneg)}"
-            f"ELb{int(fu)}EEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE")
+            "EEvjjjjiiiPKfPKN4mppi8JointDevENS2_9DevParamsE")
 
 
 # the symbols the launchers name for the shapes the benchmarks and the drop-in classes run
 EXPECTED = {
-    # (fu: the fused step, one launch per step; the two-kernel instantiations stay for peer/RCCL shards)
-    "mppi_rollout_arm.hip": [_rollout(1, 7, 1, 32, True, True, False, True, fu=True),   # arm C3, fp64 state
-                             _rollout(1, 7, 1, 32, True, True, False, True)],
-    "mppi_rollout_arm32.hip": [_rollout(1, 7, 1, 32, False, True, False, True, fu=True)],
-    "mppi_rollout_wb.hip": [_rollout(2, 10, 1, 64, False, True, False, True),         # C4 shard (peer / RCCL)
-                            _rollout(2, 10, 1, 64, False, True, False, False, fu=True),   # K=8192 fused
+    "mppi_rollout_arm.hip": [_rollout(1, 7, 1, 32, True, True, False, True)],        # arm C3, fp64 state
+    "mppi_rollout_arm32.hip": [_rollout(1, 7, 1, 32, False, True, False, True)],
+    "mppi_rollout_wb.hip": [_rollout(2, 10, 1, 64, False, True, False, True),         # C4 shard
                             _rollout(2, 10, 1, 64, False, True, False, False)],       # K=65536
-    "mppi_rollout_drone.hip": [_rollout(0, 3, 1, 32, False, True, False, True, fu=True)],
+    "mppi_rollout_drone.hip": [_rollout(0, 3, 1, 32, False, True, False, True)],
     "mppi_rollout_quad.hip": ["_Z14k_rollout_quadILb1ELb0ELi1ELi512EEvjjjjiiPKfN4mppi9DevParamsE"],
     "mppi_finalize.hip": ["_Z10k_finalizeILi32ELi9ELi512EEvPKfS1_PKN4mppi7FinTailEjjiiiiijNS2_9FinParamsE",
                           "_Z10k_finalizeILi16ELi9ELi256EEvPKfS1_PKN4mppi7FinTailEjjiiiiijNS2_9FinParamsE"],

@@ -59,9 +59,7 @@ def _connect_self(e):
 def test_peer_one_rank_equals_unsharded(dispatch, monkeypatch):
     """(a) at the C4 shard shape (whole-body K=8192 H=64)."""
     monkeypatch.setenv("MPPI_DISPATCH", dispatch)
-    monkeypatch.setenv("MPPI_FUSED", "0")   # the unsharded TWO-kernel step: the peer step's own kernels
     plain = _engine(n_samples=8192)
-    monkeypatch.delenv("MPPI_FUSED")
     peer = _engine(n_samples=8192)
     _connect_self(peer)
     rng = np.random.default_rng(5)
@@ -95,17 +93,13 @@ def test_peer_one_rank_equals_unsharded(dispatch, monkeypatch):
     ("drone", dict(n_samples=2048, n_horizon=100, savgol_window=31), [0.1, -0.2, 1.0, 0.0, 0.0, 0.0]),
     ("quadrotor", dict(n_samples=1024, n_horizon=32), [0.0, 0.0, 1.0] + [0.0] * 9),
 ])
-def test_peer_one_rank_equals_unsharded_models(model, kw, state, monkeypatch):
+def test_peer_one_rank_equals_unsharded_models(model, kw, state):
     """(a) for the other kernel families and the widest SavGol window (a 38-column finalize
     window: the exchange's full 64-column word block), native batches and control calls."""
     from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
     st = np.array(state, np.float64)
     engines = []
-    for i in range(2):
-        if i == 0:   # the unsharded TWO-kernel step (the peer step runs k_rollout + k_finalize too)
-            monkeypatch.setenv("MPPI_FUSED", "0")
-        else:
-            monkeypatch.delenv("MPPI_FUSED")
+    for _ in range(2):
         e = Engine(make_config(model=model, seed=SEED, **kw))
         if model == "drone" or model == "quadrotor":
             e.set_target([1.0, 2.0, 3.4])

@@ -16,8 +16,6 @@ probes:
                                  per-wave phase timelines of the last rollout (stamps build,
                                  MPPI_STAMPS=1): shader clock, wave lifetimes, per-XCD / per-CU ends
   latency [model] [K] [H]        control-call latency split: enqueue vs read_outputs, flag vs event wait
-  fused [reps] [n]               the fused step (one launch) vs rollout + finalize: event-timed loops
-                                 and native batches, per shape
   rate [model] [K] [H] [calls]   control-call latency vs the idle gap before each call (100 Hz node):
                                  back to back, 10 ms sleep, 10 ms host spin, 1 ms, 0.1 ms
 """
@@ -478,63 +476,7 @@ def probe_rate(model="arm", K="4096", H="32", calls="200"):
     e.close()
 
 
-def probe_fused(reps="7", n="300"):
-    """The fused step (one k_rollout launch that finalises the step) against the two-kernel step on
-    the same engine: n fused launches and n (rollout, finalize) pairs back to back, event-timed
-    (mppi_debug_fused_timing), median of reps; then the whole native batch per step both ways
-    (MPPI_FUSED=0 engine vs default) after a 15 ms heat-up."""
-    import torch
-    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
-    L = None
-    shapes = [("arm", 4096, 32, 1), ("drone", 4096, 32, 1), ("wholebody", 8192, 64, 1), ("wholebody", 65536, 64, 1),
-              ("wholebody", 8192, 64, 8), ("arm", 1024, 32, 1)]
-    for model, K, H, V in shapes:
-        e = _engine(model=model, K=K, H=H, seed=3, n_vehicles=V) if V == 1 else None
-        if e is None:
-            e = Engine(make_config(model, device=0, n_samples=K, n_horizon=H, n_vehicles=V, seed=3))
-            for v in range(V):
-                e.set_target(*ARM_T, vehicle=v)
-            e.set_state(np.tile(np.array(STATES[model], np.float64), (V, 1)))
-        L = e._L
-        L.mppi_debug_fused_timing.restype = C.c_int
-        L.mppi_debug_fused_timing.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
-        fu, pr = C.c_double(), C.c_double()
-        fs, ps = [], []
-        for _ in range(int(reps)):
-            assert L.mppi_debug_fused_timing(e._h, int(n), C.byref(fu), C.byref(pr)) == 0, L.mppi_last_error()
-            fs.append(fu.value)
-            ps.append(pr.value)
-        e.close()
-        # native batches, both ways
-        batch = {}
-        for tag, env in (("two-kernel", "0"), ("fused", None)):
-            if env:
-                os.environ["MPPI_FUSED"] = env
-            else:
-                os.environ.pop("MPPI_FUSED", None)
-            e = Engine(make_config(model, device=0, n_samples=K, n_horizon=H, n_vehicles=V, seed=3,
-                                   state_f64=(model == "arm")))
-            for v in range(V):
-                e.set_target(*ARM_T, vehicle=v)
-            e.set_state(np.tile(np.array(STATES[model], np.float64), (V, 1)))
-            ts = []
-            for _ in range(int(reps)):
-                e.run_steps(max(200, int(15000 / (np.median(ps) + 1e-9))))
-                e.synchronize()
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                e.run_steps(int(n))
-                e.synchronize()
-                ts.append((time.perf_counter() - t0) / int(n) * 1e6)
-            batch[tag] = (float(np.median(ts)), e.dispatch_info())
-            e.close()
-        os.environ.pop("MPPI_FUSED", None)
-        print(f"{model} K={K} H={H} V={V}: events fused {np.median(fs):.2f} us vs rollout+finalize {np.median(ps):.2f} us "
-              f"| native batch per step: fused {batch['fused'][0]:.2f} us vs two-kernel {batch['two-kernel'][0]:.2f} us "
-              f"[{batch['fused'][1]}]", flush=True)
-
-
-PROBES = {"timeline": probe_timeline, "fused": probe_fused, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
+PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
           "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate}
 
