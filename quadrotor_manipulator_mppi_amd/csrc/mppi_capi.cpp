@@ -1033,6 +1033,12 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     std::memset(&f, 0, sizeof(f));
     f.model = c.model; f.V = e->V; f.H = H; f.A = e->A; f.nq = e->nq; f.qoff = e->qoff;
     f.state_f64 = c.state_f64; f.P = P;
+    // (diagnostics: MPPI_FIN_TSZ = t per finalize slice, for the slice-count / fetch trade-off
+    // measured in profiles/r05/finalize_fetch; 8 is the measured best)
+    if (const char* z = getenv("MPPI_FIN_TSZ")) {
+        const int tz = atoi(z);
+        if (tz >= 1 && tz + 2 * (c.savgol_window / 2) <= 64) e->fin_tsz = tz;
+    }
     f.tsz = e->fin_tsz; f.ts = e->fin_ts = (H + e->fin_tsz - 1) / e->fin_tsz;
     f.window = c.savgol_window; f.half = c.savgol_window / 2;
     for (int j = 0; j < c.savgol_window; ++j) f.sg[j] = e->sg_taps[c.savgol_window - 1 - j];

@@ -452,6 +452,20 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 #define STAMPRT(i) do { } while (0)
 #endif
 
+// Static instruction-mix sections (diagnostic builds, -DMPPI_SECTIONS; tools/isa_sections.py):
+// a named comment in the listing with scheduling barriers on both sides, so no instruction moves
+// across it.  Compiled out otherwise.
+#ifdef MPPI_SECTIONS
+#define SECTION(name)                                        \
+    do {                                                     \
+        __builtin_amdgcn_sched_barrier(0);                   \
+        asm volatile("; MPPI_SECTION " name ::: "memory");   \
+        __builtin_amdgcn_sched_barrier(0);                   \
+    } while (0)
+#else
+#define SECTION(name) do { } while (0)
+#endif
+
 // Inclusive fp32 segment sum (cost reduction; order-insensitive at tolerance).
 template <int L>
 __device__ __forceinline__ float seg_scan_f32(float x) {
@@ -717,12 +731,14 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     STAMPW(9);
     // the first group's standard normals overlap the loads above
     float z0[NCH][NA];
+    SECTION("prologue_philox");
     if (noise_mode != MPPI_NOISE_INJECTED) {
         const uint32_t kg = k_off + (uint32_t)((blockIdx.x * nw + wid) * R + sub);
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
             draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), vkey, step_ctr, seed_lo, seed_hi);
     }
+    SECTION("prologue_staging");
     STAMP(10);
     asm volatile("" :: "s"(kwarm));
 #pragma unroll
@@ -786,6 +802,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     // no loop-invariant hoisting of address math / key schedules into SGPRs.
     auto group = [&](const int it) __attribute__((always_inline)) {   // (the NCH = 4 extended kernel called it out of line: a 1.7 KB stack frame)
         asm volatile("" ::: "memory");   // keep LDS constant reads inside the group
+        SECTION("noise");
         // group it of block b: groups b, b + nb, ...  All blocks' groups of one iteration are
         // consecutive, so the grid's concurrent trajectory stores stay in one region of the planes
         // (consecutive groups per block scattered them: whole-body K=65536 85.5 -> 106-110 us)
@@ -882,6 +899,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             }
         }
         if (it == 0) STAMP(2);
+        SECTION("integrator");
 
         // ---- A3: double integrator (standard_normal_noise.py:41-48).  Both cumsums
         //      are fp32 Kogge-Stone scans over DPP: they sum small increments
@@ -945,6 +963,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             }
         }
         if (it == 0) STAMP(3);
+        SECTION("fk_chain");
         if (ONEG && MPPI_PRIO) set_wave_prio(2);   // progress priority (single group): see below
 
         // eps is read again only by the softmin accumulate at the end of the group: park
@@ -1049,7 +1068,9 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
                 // addresses per lane would otherwise become two vector loads in the FK
                 const float wsp = uniform_f32(p.w_sp), wso = uniform_f32(p.w_so), wtp = uniform_f32(p.w_tp),
                             wto = uniform_f32(p.w_to);
+                SECTION("pose_cost");
                 x = (MPPI_KO & 8) ? T.m[3] + T.m[7] + T.m[11] + T.m[0] : pose_cost(T, vc, term ? wtp : wsp, term ? wto : wso);
+                SECTION("traj_ee_stores");
                 if (stv) {
 #pragma unroll
                     for (int i = 0; i < 12; ++i) traj_store(trs, toff, (uint32_t)(NA + i) * plane_b, T.m[i]);
@@ -1080,6 +1101,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             }
         }
         if (it == 0) STAMP(4);
+        SECTION("cost_sum_softmin");
         if (ONEG && MPPI_PRIO) set_wave_prio(1);
 
         // ---- S_k = fl(ws * sum_{t<H-1} x_t) + fl(wt * x_{H-1}) per segment (wave-uniform picks)
@@ -1179,6 +1201,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         if (MPPI_PRIO) set_wave_prio(0);
     }
     STAMP(5);
+    SECTION("block_combine_record");
 
     // ---- cross-wave combine in LDS -> one partial record per block, one barrier:
     //      after the barrier every record thread takes rho_b = min of the 8 wave slots'

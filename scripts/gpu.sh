@@ -73,7 +73,7 @@ peer2() {   # the N>1 bench path through the peer exchange, 2 ranks on this one 
   MPPI_DIST_BACKEND=gloo MPPI_EXCHANGE=peer timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 50 --warmup 10 \
       --latency-steps 20 > $out/bench_peer2.json 2> $out/bench_peer2.err || fail "peer rehearsal" $? $out/bench_peer2.err
-  python3 -c "import json;d=json.load(open('$out/bench_peer2.json'));m=d['multi_gpu'];c=(d.get('secondary') or {}).get('c4') or {};print('peer2', d['config']['workload'], d['config']['parallelism'], 'step %.2f us'%(d['ms_per_step']*1e3), m['exchange'], m['native_comm_error'], '| c4', c.get('exchange'), ('step %.2f us'%(c.get('ms_per_step', 0)*1e3)) if c else None)"
+  python3 -c "import json;d=json.load(open('$out/bench_peer2.json'));m=d['multi_gpu'];c=(d.get('secondary') or {}).get('c4') or {};print('peer2', d['config']['workload'], d['config']['parallelism'], 'step %.2f us'%(d['ms_per_step']*1e3), m['exchange'], m['native_comm_error'], '| c4', c.get('exchange'), ('step %.2f us'%(c.get('ms_per_step', 0)*1e3)) if c else None, '| fleet_c5', {k: f.get(k) for k in ('n_gpus', 'exchange', 'vehicles_per_gpu', 'vehicles_total', 'ms_per_step', 'value')} if (f := (d.get('secondary') or {}).get('fleet_c5')) else None)"
 }
 
 case $cmd in

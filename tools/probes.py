@@ -18,6 +18,7 @@ probes:
   latency [model] [K] [H]        control-call latency split: enqueue vs read_outputs, flag vs event wait
   rate [model] [K] [H] [calls]   control-call latency vs the idle gap before each call (100 Hz node):
                                  back to back, 10 ms sleep, 10 ms host spin, 1 ms, 0.1 ms
+  store_floor [sizes] [launches] write-only floor (torch fill_) at the rollouts' per-launch bytes
 """
 import ctypes as C
 import json
@@ -476,9 +477,38 @@ def probe_rate(model="arm", K="4096", H="32", calls="200"):
     e.close()
 
 
+def probe_store_floor(sizes="1589248,9981952,46170112,369360896", launches="400"):
+    """Write-only floor at the rollout's per-launch byte counts (drone C2, arm C3, whole-body C4
+    share, fleet C5 share): torch fill_ of a buffer of that many bytes, `launches` back to back
+    between one event pair (steps-only, like the rollout's rocprof average), median of 7.  A store
+    kernel of the same size cannot finish faster on this box, so rollout_us / floor_us is how far the
+    rollout sits from its own store floor (the 8 TB/s peak is not reachable by a write stream)."""
+    import torch
+    n = int(launches)
+    for nbytes in (int(s) for s in sizes.split(",")):
+        buf = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda:0")
+        for _ in range(50):
+            buf.fill_(1.0)
+        torch.cuda.synchronize()
+        us = []
+        for trial in range(7):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for i in range(n):
+                buf.fill_(float(i))
+            b.record()
+            b.synchronize()
+            us.append(a.elapsed_time(b) * 1e3 / n)
+        m = float(np.median(us))
+        print(f"store floor {nbytes / 1e6:8.2f} MB: {m:7.2f} us/launch  {nbytes / m / 1e3:7.1f} GB/s  "
+              f"(median of 7 x {n} launches)", flush=True)
+        del buf
+
+
 PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
-          "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate}
+          "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate,
+          "store_floor": probe_store_floor}
 
 if __name__ == "__main__":
     if len(sys.argv) < 2 or sys.argv[1] not in PROBES:
