@@ -9,7 +9,7 @@ Every test runs twice:
 * ``committed`` -- against the committed fixtures.  They were made on another
   host; torch's vectorised transcendentals and reductions differ across CPU
   microarchitectures by an ulp or so (measured: norm-wise <= 6e-7, see
-  DESIGN.md §5), so these checks hold the oracle to CROSS_HOST_RTOL of each
+  DESIGN.md §6), so these checks hold the oracle to CROSS_HOST_RTOL of each
   array's largest magnitude.  Bit-exact where the host is the one that made them.
 
 Unless a comment says otherwise.  CPU only.

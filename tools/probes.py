@@ -61,7 +61,7 @@ def probe_timeline(name, trials="30"):
     se = ShardedEngine(seed=1234, native=native, **w)
     eng = se.engine
     V = w.get("n_vehicles", 1)
-    bench.set_targets(eng, w["model"], V)
+    bench.set_targets(eng, w["model"], se.vehicles)
     eng.set_state(bench.make_state(w["model"], V))
     L = eng._L
     L.mppi_debug_stamps.restype = C.c_int64
@@ -116,8 +116,10 @@ def probe_timeline(name, trials="30"):
                 fx = f[:, 15] & 0xF
                 for c in range(8):
                     m = fx == c
-                    if m.any():
+                    if m.any():   # per XCD: first block start, last records-combined, last end
                         row[f"{key}_xcd{c}_start"] = (f[m, 13].min() - t0) * 10.0
+                        row[f"{key}_xcd{c}_records"] = (f[m, 1].max() - t0) * 10.0
+                        row[f"{key}_xcd{c}_end"] = (f[m, 14].max() - t0) * 10.0
         rows.append(row)
     med = {k: float(np.median([r[k] for r in rows if k in r])) for k in rows[0].keys()}
     out = {"workload": name, "trials": trials, "dispatch": eng.dispatch_info(),
