@@ -7,9 +7,15 @@
 //   hipcc --offload-arch=gfx950 -O3 -o tools/_bin/cp_hop_probe tools/cp_hop_probe.hip
 //   tools/_bin/cp_hop_probe [iterations]
 //
+// Part 3 replaces B's kernel with the real collective: a 1-rank RCCL communicator's
+// ncclAllReduce of the C4 shard's 660-float slot (librccl.so.1 by dlopen, as the engine loads it).
+//
 // Stamps are s_memrealtime (100 MHz).  Every spin has a 20 ms deadline, so a lost release ends
 // the kernel (reported as a timeout) instead of hanging the GPU.
 #include <hip/hip_runtime.h>
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -72,6 +78,7 @@ int main(int argc, char** argv) {
     CK(hipMemset(t, 0, 64 * sizeof(u64)));
     CK(hipDeviceSynchronize());
     u64 h[64];
+    u64* hbuf = h;
 
     // 1. the plain boundary: two kernels back to back on one stream
     std::vector<double> bnd;
@@ -106,6 +113,52 @@ int main(int argc, char** argv) {
         report("B's kernel start -> WriteValue -> A sees", back_us);
         report("round trip (A signals .. A released)", total);
     }
+
+    // 3. the same round trip with the 1-rank all-reduce in place of B's kernel
+    void* lib = dlopen("librccl.so.1", RTLD_NOW);
+    if (!lib) lib = dlopen("librccl.so", RTLD_NOW);
+    if (!lib) { printf("librccl not loadable: %s\n", dlerror()); return 0; }
+    auto get_id = (ncclResult_t(*)(ncclUniqueId*))dlsym(lib, "ncclGetUniqueId");
+    auto init = (ncclResult_t(*)(ncclComm_t*, int, ncclUniqueId, int))dlsym(lib, "ncclCommInitRank");
+    auto ar = (ncclResult_t(*)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t))dlsym(lib, "ncclAllReduce");
+    auto destroy = (ncclResult_t(*)(ncclComm_t))dlsym(lib, "ncclCommDestroy");
+    if (!get_id || !init || !ar || !destroy) { printf("librccl lacks an entry point\n"); return 0; }
+    ncclUniqueId id;
+    ncclComm_t comm;
+    if (get_id(&id) != ncclSuccess || init(&comm, 1, id, 0) != ncclSuccess) { printf("rccl init failed\n"); return 0; }
+    float* slot = nullptr;
+    CK(hipMalloc(&slot, 660 * sizeof(float)));
+    CK(hipMemset(slot, 0, 660 * sizeof(float)));
+    for (int i = 0; i < 20; ++i) ar(slot, slot, 660, ncclFloat32, ncclSum, comm, B);   // connection setup
+    CK(hipStreamSynchronize(B));
+    std::vector<double> rt, bnd_ar;
+    timeouts = 0;
+    for (int i = iters + 1; i <= 2 * iters; ++i) {
+        CK(hipStreamWaitValue32(B, go, (uint32_t)i, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        ar(slot, slot, 660, ncclFloat32, ncclSum, comm, B);
+        CK(hipStreamWriteValue32(B, back, (uint32_t)i, 0));
+        hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, A, go, back, (uint32_t)i, t);
+        CK(hipStreamSynchronize(A));
+        CK(hipStreamSynchronize(B));
+        CK(hipMemcpy(hbuf, t, 16 * sizeof(u64), hipMemcpyDeviceToHost));
+        if (hbuf[2] < (u64)i) { ++timeouts; continue; }
+        rt.push_back((double)(hbuf[1] - hbuf[0]) * 0.01);
+    }
+    printf("timeouts (rccl): %d of %d\n", timeouts, iters);
+    if (!rt.empty()) report("round trip with ncclAllReduce (1 rank, 660 floats)", rt);
+    // the reference point: kernel -> all-reduce -> kernel on ONE stream, start of the first to start of the last
+    for (int i = 0; i < iters; ++i) {
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, B, t);
+        ar(slot, slot, 660, ncclFloat32, ncclSum, comm, B);
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, B, t + 1);
+        CK(hipStreamSynchronize(B));
+        CK(hipMemcpy(hbuf, t, 2 * sizeof(u64), hipMemcpyDeviceToHost));
+        bnd_ar.push_back((double)(hbuf[1] - hbuf[0]) * 0.01);
+    }
+    report("same stream: kernel -> ncclAllReduce -> kernel", bnd_ar);
+    destroy(comm);
+    CK(hipFree(slot));
     CK(hipFree(t));
     CK(hipFree(go));
     CK(hipFree(back));
