@@ -507,7 +507,35 @@ def probe_store_floor(sizes="1589248,9981952,46170112,369360896", launches="400"
         del buf
 
 
-PROBES = {"timeline": probe_timeline, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
+def probe_noise_src(model="arm", K="4096", H="32", n="2000"):
+    """Rollout with the noise drawn on the device (Philox + Box-Muller in the prologue) against the
+    same rollout reading its noise from HBM (the injected-noise path): n rollouts of each, back to
+    back, Philox first.  Run under `rocprofv3 --kernel-trace`: the two halves of the k_rollout
+    dispatches are the two modes (same kernel symbol).  Tells what drawing the next step's noise
+    off the critical path could save at most."""
+    import torch
+    K, H, n = int(K), int(H), int(n)
+    state = np.array(STATES[model], np.float64)
+    for mode in ("philox", "injected"):
+        e = _engine(model, K, H, noise=mode)
+        e.set_state(state)
+        A = e.A
+        eps = torch.randn(K * H * A, device="cuda:0", dtype=torch.float32) * 0.1 if mode == "injected" else None
+        torch.cuda.synchronize()
+        ptr = eps.data_ptr() if eps is not None else 0
+        for _ in range(50):
+            e.rollout(ptr)
+        e.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            e.rollout(ptr)
+        e.synchronize()
+        print(f"{model} K={K} H={H} {mode:8s}: {n} rollouts, {(time.perf_counter() - t0) / n * 1e6:.2f} us each "
+              f"(host-paced; the kernel trace has the device time)", flush=True)
+        e.close()
+
+
+PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
           "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate,
           "store_floor": probe_store_floor}
