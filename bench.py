@@ -387,13 +387,16 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     heat_ms = float(os.environ.get("MPPI_BENCH_HEAT_MS", "15"))
     n_heat = 0
     if heat_ms > 0:
-        t_step = tim["pair_us"] * 1e-6 if tim is not None else None
-        if t_step is None:   # no event timing (profiler runs): one timed 20-step batch
-            barrier()
-            t0 = time.perf_counter()
-            se.run_steps(20)
-            barrier()
-            t_step = (time.perf_counter() - t0) / 20
+        # the step's wall time from one timed 20-step batch (a host-paced step -- the torch
+        # collective's host round trip -- runs far longer than its kernel pair, and a heat-up sized
+        # from the pair ran ~0.3 s of such steps per batch), never below the kernel pair's time
+        barrier()
+        t0 = time.perf_counter()
+        se.run_steps(20)
+        barrier()
+        t_step = (time.perf_counter() - t0) / 20
+        if tim is not None:
+            t_step = max(t_step, tim["pair_us"] * 1e-6)
         t_step = reduce_max([t_step], dist, red_dev)[0]
         n_heat = int(min(20000, max(100, np.ceil(heat_ms * 1e-3 / t_step))))
     bt_cold, _ = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
