@@ -137,6 +137,7 @@ traffic)
     done
     key=$(python3 -c "import json; print(json.load(open('$d/FETCH_SIZE.json'))['roofline']['launch_shape'])") || exit 1
     python3 scripts/pmc.py traffic $d $key --merge $out/pmc_rollout.json --workload $spec || exit 1
+    rm -rf $d/FETCH_SIZE $d/WRITE_SIZE   # (the counter CSVs: gpurun copies back at most 64 MiB)
   done ;;
 *)
   sed -n '2,20p' "$0"; exit 2 ;;
