@@ -19,6 +19,10 @@ probes:
   rate [model] [K] [H] [calls]   control-call latency vs the idle gap before each call (100 Hz node):
                                  back to back, 10 ms sleep, 10 ms host spin, 1 ms, 0.1 ms
   store_floor [sizes] [launches] write-only floor (torch fill_) at the rollouts' per-launch bytes
+  noise_src [model] [K] [H] [n]  rollout with device Philox vs noise read from HBM (run under a kernel trace)
+  peer_soak [model] [K] [H] [G] [batches] [steps]
+                                 G in-process peer-exchange ranks for batches x steps: no timeout, ranks
+                                 bit-identical after every batch
 """
 import ctypes as C
 import json
@@ -419,6 +423,41 @@ def probe_peer_ranks(model="arm", K="512", H="32", Gs="1,2,4,8"):
             e.close()
 
 
+def probe_peer_soak(model="wholebody", K="8192", H="64", G="2", batches="20", steps="1000"):
+    """Soak of the peer exchange: G in-process ranks (mppi_peer_connect_ptrs) run `batches` native
+    batches of `steps` steps together; after every batch each rank's sticky timeout word must be 0
+    and every rank's u_prev bit-identical to rank 0's.  Prints one line per batch and a verdict."""
+    G, nb, ns = int(G), int(batches), int(steps)
+    es = [_engine(model=model, K=int(K), H=int(H), seed=3, shard_rank=r, shard_count=G) for r in range(G)]
+    for e in es:
+        e.peer_open()
+    addrs = [e.peer_region() for e in es]
+    for e in es:
+        e.peer_connect_ptrs(addrs)
+    ok = True
+    t_all = time.perf_counter()
+    for b in range(nb):
+        t0 = time.perf_counter()
+        for e in es:
+            e.run_steps(ns)
+        for e in es:
+            e.synchronize()
+        dt = (time.perf_counter() - t0) / ns * 1e6
+        sticky = [e.peer_status(reports=False)[0] for e in es]
+        u0 = es[0].get_u_prev()
+        same = all(np.array_equal(u0, e.get_u_prev()) for e in es[1:])
+        fin = bool(np.isfinite(u0).all())
+        ok &= (not any(sticky)) and same and fin
+        print(f"batch {b}: {ns} steps, {dt:.2f} us/step, sticky {sticky}, ranks bit-identical {same}, finite {fin}",
+              flush=True)
+    print(f"{model} K={K} H={H} G={G}: {nb * ns} steps in {time.perf_counter() - t_all:.1f} s: "
+          f"{'OK' if ok else 'FAILED'}", flush=True)
+    for e in es:
+        e.close()
+    if not ok:
+        sys.exit(1)
+
+
 def probe_rate(model="arm", K="4096", H="32", calls="200"):
     """Control-call latency against the idle time before each call (bench.py latency_100hz: the
     node ticks at 100 Hz, kinova.py:101).  Phases, in order: back to back; 10 ms sleeps (rospy.Rate);
@@ -535,7 +574,7 @@ def probe_noise_src(model="arm", K="4096", H="32", n="2000"):
         e.close()
 
 
-PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
+PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "peer_soak": probe_peer_soak, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
           "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate,
           "store_floor": probe_store_floor}
