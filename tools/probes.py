@@ -20,6 +20,8 @@ probes:
                                  back to back, 10 ms sleep, 10 ms host spin, 1 ms, 0.1 ms
   store_floor [sizes] [launches] write-only floor (torch fill_) at the rollouts' per-launch bytes
   noise_src [model] [K] [H] [n]  rollout with device Philox vs noise read from HBM (run under a kernel trace)
+  geom [model] [K] [H] [bpvs] [threads]
+                                 rollout / finalize / pair times per blocks-per-vehicle choice
   peer_soak [model] [K] [H] [G] [batches] [steps]
                                  G in-process peer-exchange ranks for batches x steps: no timeout, ranks
                                  bit-identical after every batch
@@ -423,6 +425,25 @@ def probe_peer_ranks(model="arm", K="512", H="32", Gs="1,2,4,8"):
             e.close()
 
 
+def probe_geom(model="wholebody", K="8192", H="64", bpvs="256,512,1024", threads="0"):
+    """Rollout / finalize / pair times (HIP events, kernel_timing_ex, median of 7) for each
+    blocks-per-vehicle choice (the grid's groups per wave follow from it: K / (bpv * rollouts per
+    block)); one engine per choice, created in turn, both orders."""
+    res = {}
+    bl = [int(b) for b in bpvs.split(",")]
+    for order in (bl, bl[::-1]):
+        for b in order:
+            e = _engine(model, int(K), int(H), blocks_per_vehicle=b, block_threads=int(threads))
+            for _ in range(3):
+                e.kernel_timing_ex(400)
+            xs = [e.kernel_timing_ex(400) for _ in range(7)]
+            r = tuple(float(np.median([x[i] for x in xs])) for i in range(3))
+            res.setdefault(b, []).append(r)
+            print(f"{model} K={K} H={H} blocks/vehicle {b}: rollout {r[0]:.2f} us, finalize {r[1]:.2f}, "
+                  f"pair {r[2]:.2f}  [{e.dispatch_info()}]", flush=True)
+            e.close()
+
+
 def probe_peer_soak(model="wholebody", K="8192", H="64", G="2", batches="20", steps="1000"):
     """Soak of the peer exchange: G in-process ranks (mppi_peer_connect_ptrs) run `batches` native
     batches of `steps` steps together; after every batch each rank's sticky timeout word must be 0
@@ -574,7 +595,7 @@ def probe_noise_src(model="arm", K="4096", H="32", n="2000"):
         e.close()
 
 
-PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "peer_soak": probe_peer_soak, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
+PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "peer_soak": probe_peer_soak, "geom": probe_geom, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
           "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate,
           "store_floor": probe_store_floor}
