@@ -17,6 +17,15 @@
 #   scripts/gpu.sh pmc      <tag> [bench.py args]         rocprofv3 counter passes, one group per pass
 #   scripts/gpu.sh traffic  <tag> [workload[:K] ...]      FETCH_SIZE / WRITE_SIZE per launch shape ->
 #                                                         gpurun_out/traffic_<tag>/pmc_rollout.json
+#   scripts/gpu.sh counters <tag> <lib.so|prod> <workload> "<counters>" | trace ...
+#                                                         one control-steps-only rocprofv3 pass per group
+#                                                         (`trace`: a kernel trace with stats) of one build
+#                                                         and workload, summarised into summary.txt and the
+#                                                         CSVs deleted; the environment passes through
+#                                                         (e.g. MPPI_FIN_TSZ, MPPI_FIN_DEBUG=0). Used for
+#                                                         profiles/r05: finalize_fetch (RDREQ_64B/128B, SQC_*,
+#                                                         a 4-XCD build, MPPI_FIN_TSZ=8/16/32) and
+#                                                         wholebody_sections (SQ_INSTS_* per knockout build)
 #
 # Every GPU step runs under its own time limit and the first failure ends the script.
 cmd=$1; tag=${2:-dev}; shift 2
@@ -139,6 +148,31 @@ traffic)
     python3 scripts/pmc.py traffic $d $key --merge $out/pmc_rollout.json --workload $spec || exit 1
     rm -rf $d/FETCH_SIZE $d/WRITE_SIZE   # (the counter CSVs: gpurun copies back at most 64 MiB)
   done ;;
+counters)
+  lib=$1; w=$2; shift 2
+  [ "$lib" = prod ] && lib=$PWD/quadrotor_manipulator_mppi_amd/lib/libmppi_hip.so
+  i=0
+  for grp in "$@"; do
+    i=$((i+1)); d=$out/p$i
+    if [ "$grp" = trace ]; then prof="--kernel-trace --stats"; else prof="--pmc $grp --kernel-trace"; fi
+    MPPI_HIP_LIB=$lib timeout -s KILL 120 rocprofv3 $prof --output-format csv -d $d -o run -- \
+        python3 bench.py --workload $w --steps 200 --warmup 20 --latency-steps 0 --no-cpu-baseline \
+        --no-kernel-timing --secondary "" > $d.json 2> $d.err || fail "pass $i ($grp)" $? $d.err
+    echo "== $w $(basename $lib) pass $i ($grp)" >> $out/summary.txt
+    if [ "$grp" = trace ]; then
+      python3 - "$d/run_kernel_stats.csv" >> $out/summary.txt <<'PY' || exit 1
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "k_rollout" in r["Name"] or "k_finalize" in r["Name"]:
+        print("   steps-only", r["Name"].split("(")[0], r["Calls"], "avg ns", r["AverageNs"])
+PY
+    else
+      python3 scripts/pmc.py summary $d >> $out/summary.txt || exit 1
+    fi
+    rm -rf $d   # (the CSVs: gpurun copies back at most 64 MiB)
+    echo "pass $i ($grp) ok"
+  done
+  grep -v "copyBuffer\|fillBuffer" $out/summary.txt ;;
 *)
-  sed -n '2,20p' "$0"; exit 2 ;;
+  sed -n '2,29p' "$0"; exit 2 ;;
 esac
