@@ -427,10 +427,14 @@ __device__ __forceinline__ float pose_cost(const Mat34& T, const VehicleConst& v
 #elif defined(MPPI_STAMPS)   // MPPI_TIMELINE: wall-clock time at wave start / end and at three phase
                              // boundaries (after the first group's Philox: slot 10, after the
                              // prologue's barrier: slot 1, after the rollout groups: slot 5), no
-                             // waits: the kernel's own schedule
+                             // waits: the kernel's own schedule; -DMPPI_TIMELINE_FINE=1 stamps every
+                             // phase boundary (tools/probes.py timeline prints the per-phase medians)
+#ifndef MPPI_TIMELINE_FINE
+#define MPPI_TIMELINE_FINE 0
+#endif
 #define STAMP(i)                                                                                      \
     do {                                                                                              \
-        if (((i) == 1 || (i) == 5 || (i) == 10) && pk.stamps && lane == 0) {                          \
+        if (((i) == 1 || (i) == 5 || (i) == 10 || MPPI_TIMELINE_FINE) && pk.stamps && lane == 0) {    \
             const size_t w_ = ((size_t)blockIdx.y * p.nb + blockIdx.x) * nw + wid;        \
             pk.stamps[w_ * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();                         \
         }                                                                                             \

@@ -102,6 +102,13 @@ def probe_timeline(name, trials="30"):
                "roll_staging_med": float(np.median(r[:, 1] - r[:, 10])) * 10.0,
                "roll_groups_med": float(np.median(r[:, 5] - r[:, 1])) * 10.0,
                "roll_combine_med": float(np.median(r[:, 14] - r[:, 5])) * 10.0}
+        if (r[:, 3] > 0).all():   # a -DMPPI_TIMELINE_FINE=1 build: every phase boundary stamped
+            chain = [(13, "start"), (9, "loads_issued"), (10, "philox"), (8, "staging_stores"), (1, "barrier"),
+                     (2, "noise"), (3, "integrator"), (4, "fk_cost_stores"), (5, "cost_sum_softmin"),
+                     (11, "lds_deposit"), (6, "combine_barrier"), (12, "cost_stores_fw"), (7, "record_body"),
+                     (14, "end")]
+            for (a, _), (b, nm) in zip(chain, chain[1:]):
+                row[f"phase_{nm}_med"] = float(np.median(r[:, b] - r[:, a])) * 10.0
         for c in range(8):
             m = xcc == c
             if m.any():
