@@ -517,3 +517,20 @@ def test_vehicle_split_two_processes_equal_one_engine():
     assert all(r[6].startswith("aql;") for r in res), [r[6] for r in res]
     assert np.array_equal(np.concatenate([r[4] for r in res]), u_f)
     assert np.array_equal(np.concatenate([r[5] for r in res]), o_f)
+
+
+def test_vehicle_offset_range():
+    """The fleet-wide vehicle index rides in the noise argument's high half: an engine whose last
+    vehicle is fleet vehicle 32767 is accepted and steps to finite outputs; one past it, or a
+    negative offset, is rejected at create (MPPI_ERR_INVALID_ARG)."""
+    from quadrotor_manipulator_mppi_amd._capi import MPPIError
+    V, K, H = 2, 256, 64
+    e = _fleet_engine(V, K, H, offset=32768 - V)
+    _set_fleet_targets(e, range(V))
+    e.set_state(_fleet_state(V))
+    out, u0, st = e.step(_fleet_state(V))
+    assert np.isfinite(out).all() and np.isfinite(u0).all() and not any(s.nonfinite for s in st)
+    e.close()
+    for bad in (32768 - V + 1, -1):
+        with pytest.raises(MPPIError):
+            _fleet_engine(V, K, H, offset=bad)
