@@ -56,7 +56,10 @@
 #ifndef MPPI_S_PLAIN
 #define MPPI_S_PLAIN 0
 #endif
-// park eps in LDS across the FK and cost (k_rollout, NA >= 7)
+// park eps in LDS across the FK and cost (k_rollout, NA >= 7) -- in the extended and the
+// multi-chunk kernels only: the common one-chunk kernels keep it in registers (whole-body 89 -> 96
+// VGPRs, still 5 waves per SIMD, no scratch; same-process A/B, mean of both orders,
+// profiles/r05/eps_stash: C3 -0.10 us per step, whole-body K=8192 -0.22, K=65536 -1.7, V=8 fleet -1.7)
 #ifndef MPPI_EPS_STASH
 #define MPPI_EPS_STASH 1
 #endif
@@ -974,7 +977,7 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
         // it in this wave's LDS slot (the integrator is done with it; each lane its own
         // row, so no hand-off) across the FK and cost, the kernel's register peak.  The
         // compiler barriers stop it from forwarding the stored values in registers.
-        constexpr bool kStash = MPPI_EPS_STASH && NA >= 7;
+        constexpr bool kStash = MPPI_EPS_STASH && NA >= 7 && (XC || NCH > 1);
         constexpr int kESP = (NCH == 1) ? IntegGeom<LSEG, NA>::P : NA;   // row pitch (odd for NCH == 1)
         if constexpr (kStash) {
 #pragma unroll
