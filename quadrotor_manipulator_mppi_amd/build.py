@@ -31,7 +31,11 @@ _ASAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-po
 # noise mode, H, u_prev, joint table; finalize: record and tail pointers, sizes, sequence)
 # are preloaded into SGPRs at wave launch.
 _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
+# the C3 unit (arm, fp64 state, H <= 32) with the max-ilp scheduler: its single-group kernel is one
+# wave's dependent chain (mppi_rollout_arm_h32.hip; profiles/r05/sched_maxilp)
+_MAXILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
+           ("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP),
            ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=14"]),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
 HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",

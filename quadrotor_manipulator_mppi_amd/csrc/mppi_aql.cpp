@@ -95,7 +95,8 @@ hsa_status_t pick_pool(hsa_amd_memory_pool_t pool, void* data) {
 std::mutex g_mu;
 std::map<int, Device> g_dev;
 
-const char* const kUnits[] = {"mppi_rollout_drone", "mppi_rollout_arm", "mppi_rollout_arm32", "mppi_rollout_wb",
+const char* const kUnits[] = {"mppi_rollout_drone", "mppi_rollout_arm", "mppi_rollout_arm_h32", "mppi_rollout_arm32",
+                              "mppi_rollout_wb",
                               "mppi_rollout_quad", "mppi_finalize"};
 
 std::string hsa_msg(hsa_status_t s) {

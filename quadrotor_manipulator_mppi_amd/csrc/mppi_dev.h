@@ -252,6 +252,7 @@ struct FinParams {
 extern "C" {
 int mppi_launch_rollout(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_arm64(const mppi::DevParams* p, int block_threads, void* stream);
+int mppi_launch_rollout_arm64_h32(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_arm32(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_wb(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_quad(const mppi::DevParams* p, int block_threads, void* stream);

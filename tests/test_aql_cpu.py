@@ -38,7 +38,8 @@ def _rollout(model, na, nch, lseg, f64, vone, xc, oneg):
 
 # the symbols the launchers name for the shapes the benchmarks and the drop-in classes run
 EXPECTED = {
-    "mppi_rollout_arm.hip": [_rollout(1, 7, 1, 32, True, True, False, True)],        # arm C3, fp64 state
+    "mppi_rollout_arm_h32.hip": [_rollout(1, 7, 1, 32, True, True, False, True)],    # arm C3, fp64 state
+    "mppi_rollout_arm.hip": [_rollout(1, 7, 1, 64, True, True, False, True)],        # arm H = 64, fp64 state
     "mppi_rollout_arm32.hip": [_rollout(1, 7, 1, 32, False, True, False, True)],
     "mppi_rollout_wb.hip": [_rollout(2, 10, 1, 64, False, True, False, True),         # C4 shard
                             _rollout(2, 10, 1, 64, False, True, False, False)],       # K=65536
