@@ -31,12 +31,17 @@ _ASAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-po
 # noise mode, H, u_prev, joint table; finalize: record and tail pointers, sizes, sequence)
 # are preloaded into SGPRs at wave launch.
 _ROLL = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-kernarg-preload-count=11"]
-# the C3 unit (arm, fp64 state, H <= 32) with the max-ilp scheduler: its single-group kernel is one
-# wave's dependent chain (mppi_rollout_arm_h32.hip; profiles/r05/sched_maxilp)
-_MAXILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-SOURCES = [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
-           ("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP),
-           ("mppi_rollout_wb.hip", _ROLL), ("mppi_rollout_quad.hip", _ROLL), ("mppi_finalize.hip", ["-mllvm", "-amdgpu-kernarg-preload-count=14"]),
+# the C3 unit (arm, fp64 state, H <= 32) and the 6-DoF quadrotor unit with the max-ilp scheduler:
+# both kernels are one wave's dependent chain (profiles/r05/sched_maxilp: C3 -0.28 us, quadrotor
+# K=4096 H=32 -0.25 us, K=65536 -0.8..-1.4 us; on the other units it measured mixed or slower)
+_MAXILP = ["-mllvm", "-amdgpu-sched-strategy=" + os.environ.get("MPPI_C3_SCHED", "max-ilp")]   # (knob: experiments)
+_FIN = ["-mllvm", "-amdgpu-kernarg-preload-count=14"]
+# (experiments: MPPI_MAXILP_UNITS = extra units built with max-ilp, comma-separated)
+_XI = [u for u in os.environ.get("MPPI_MAXILP_UNITS", "").split(",") if u]
+SOURCES = [(u, f + (_MAXILP if u in _XI else [])) for u, f in
+           [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
+            ("mppi_rollout_wb.hip", _ROLL), ("mppi_finalize.hip", _FIN)]] + \
+          [("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP), ("mppi_rollout_quad.hip", _ROLL + _MAXILP),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
 HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",
            os.path.join("..", "..", "include", "mppi_hip.h")]
