@@ -41,7 +41,7 @@ _XI = [u for u in os.environ.get("MPPI_MAXILP_UNITS", "").split(",") if u]
 SOURCES = [(u, f + (_MAXILP if u in _XI else [])) for u, f in
            [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
             ("mppi_rollout_wb.hip", _ROLL), ("mppi_finalize.hip", _FIN)]] + \
-          [("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP), ("mppi_rollout_quad.hip", _ROLL + _MAXILP),
+          [("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP + os.environ.get("MPPI_C3_EXTRA", "").split()), ("mppi_rollout_quad.hip", _ROLL + _MAXILP),
            ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
 HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",
            os.path.join("..", "..", "include", "mppi_hip.h")]
