@@ -841,10 +841,10 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     // auto: one block per group (iters == 1: the single-group kernel) while the grid is at
     // most 512 blocks (2 per CU); above that >= 2 groups per block (the looping kernel; the
     // prologue and the block combine are amortised, fewer records for the finalize),
-    // capped at 1024 blocks in total.  Measured on MI355X (tools/geom_sweep.py,
-    // tools/ab_interleave.py): WB K=8192 15.0 us at 512 looping blocks vs
-    // 16.3 at 1024 single-group blocks (8 waves/SIMD) -- whose finalize also reads twice
-    // the records (7.4 vs 5.6 us); K=65536 best at 1024; V=8 fleet at 128/vehicle.
+    // capped at 1024 blocks in total.  Re-measured on MI355X in round 5 (tools/probes.py geom,
+    // profiles/r05/geom): WB K=8192 step pair 17.6 us at 512 looping blocks vs 19.5-20.7 at 1024
+    // single-group blocks (whose finalize also reads twice the records) and 18.3 at 256; K=65536
+    // best at 1024 (85.2-86.1 us pairs vs 87.6-92.9 at 512, 89.1+ with 256-thread blocks).
     if (nb <= 0) {
         nb = (groups * e->V <= 512) ? groups : std::min(std::max(1, groups / 2), std::max(1, 1024 / e->V));
     }
