@@ -419,6 +419,11 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
             lat.append(time.perf_counter() - t1)
     eng.synchronize()
     lat100 = latency_at_rate(se, state, lat_rate_calls) if lat_rate_calls else []
+    lat100k = []
+    if lat_rate_calls:   # the same cadence with the engine's keep-alive on (mppi_set_keepalive, 1 ms)
+        eng.set_keepalive(1000)
+        lat100k = latency_at_rate(se, state, lat_rate_calls)
+        eng.set_keepalive(0)
     if not lat and not lat100:
         se.step(state)
     dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
@@ -427,6 +432,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.mode == "rccl" else None
     res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
+           "lat100_keepalive": lat100k,
            "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
            "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
@@ -536,6 +542,7 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
         "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
         "latency_100hz": latency_100hz(r.get("lat100"), lat),
+        "latency_100hz_keepalive": latency_100hz(r.get("lat100_keepalive"), lat, keepalive_us=1000),
         "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
         "roofline": rf,
         "cpu_baseline": cpu,
@@ -564,18 +571,22 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
     return line
 
 
-def latency_100hz(lat100, lat_b2b):
-    """The control call at the node's 100 Hz cadence (latency_at_rate) beside the back-to-back one."""
+def latency_100hz(lat100, lat_b2b, keepalive_us=0):
+    """The control call at the node's 100 Hz cadence (latency_at_rate) beside the back-to-back one;
+    with ``keepalive_us`` the engine's keep-alive (mppi_set_keepalive) ran during the idle gaps."""
     if not lat100:
         return None
     x = np.array(lat100) * 1e3
     p50 = float(np.median(x))
     b2b = float(np.median(lat_b2b)) if len(lat_b2b) else None
+    what = ("host-inclusive control call (state in, outputs, check_reach) started on every 10 ms tick after "
+            "100 ms idle, no heat-up: the arm node's rospy.Rate(100) loop (kinova.py:101); the GPU idles "
+            "~10 ms between calls")
+    if keepalive_us:
+        what += f"; the engine's keep-alive on: a one-wave kernel every {keepalive_us} us of idle (mppi_set_keepalive)"
     return {"p50_ms": p50, "p99_ms": float(np.percentile(x, 99)), "mean_ms": float(x.mean()), "calls": int(x.size),
-            "period_ms": 10.0, "vs_back_to_back_p50": p50 / b2b if b2b else None,
-            "what": "host-inclusive control call (state in, outputs, check_reach) started on every 10 ms tick after "
-                    "100 ms idle, no heat-up: the arm node's rospy.Rate(100) loop (kinova.py:101); the GPU idles "
-                    "~10 ms between calls"}
+            "period_ms": 10.0, "vs_back_to_back_p50": p50 / b2b if b2b else None, "keepalive_us": keepalive_us,
+            "what": what}
 
 
 def secondary_entry(s, ns):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 7
+#define MPPI_ABI_VERSION 8
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_PEER_HANDLE_BYTES 64  /* hipIpcMemHandle_t */
 #define MPPI_MAX_ACTION 16
@@ -345,6 +345,17 @@ mppi_status mppi_run_steps(mppi_engine* e, int32_t n);
 mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len);
 
 mppi_status mppi_synchronize(mppi_engine* e);
+
+/* Keep-alive for a controller that ticks with idle gaps (the arm node's rospy.Rate(100) loop,
+ * kinova.py:101; no reference counterpart -- the reference's torch calls pay the same wake-up): while
+ * period_us > 0, a host thread of the engine launches a one-wave kernel on its own stream every
+ * period_us during which no mppi_step / mppi_run_steps started, so the GPU, its queues and the
+ * host link stay out of their idle states between ticks.  It touches no engine state (results are
+ * unchanged) and costs one tiny kernel per period.  period_us: 0 = off (the default), else
+ * 100 .. 1000000.  mppi_destroy stops it.  mppi_get_keepalive: the period and the kernels
+ * launched so far. */
+mppi_status mppi_set_keepalive(mppi_engine* e, int32_t period_us);
+mppi_status mppi_get_keepalive(mppi_engine* e, int32_t* period_us, int64_t* launches);
 
 /* Readback in the reference's layouts (synchronous):
  *   costs    S (V,K)                         compute_all_cost()

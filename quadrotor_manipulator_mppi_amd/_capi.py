@@ -21,7 +21,7 @@ NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM, ERR_PEER_TIMEOUT = 0, -1, -2, -3, -4, -5, -6
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_PEERS = 8
 COMM_ID_BYTES = 128
 PEER_HANDLE_BYTES = 64
@@ -117,6 +117,8 @@ PROTOTYPES = {
     "mppi_run_steps": (_ST, [_P, C.c_int32]),
     "mppi_dispatch_info": (_ST, [_P, C.c_char_p, C.c_int32]),
     "mppi_synchronize": (_ST, [_P]),
+    "mppi_set_keepalive": (_ST, [_P, C.c_int32]),
+    "mppi_get_keepalive": (_ST, [_P, _I32, C.POINTER(C.c_int64)]),
     "mppi_get_costs": (_ST, [_P, _F]),
     "mppi_get_weights": (_ST, [_P, _F]),
     "mppi_get_noise": (_ST, [_P, _F]),

@@ -12,11 +12,13 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -413,6 +415,17 @@ struct mppi_engine {
     bool aql_call = false;              // ... from a native control call (flags carry bit 31)
     bool calls_native = false;          // the last mppi_step went out as native packets
     double call_wait_us = 0.0;          // diagnostics (MPPI_AQL_PROFILE): the last call's flag wait
+    // keep-alive (mppi_set_keepalive): a host thread launches k_keepalive on its own stream every
+    // keep_us while no control call or batch has started for that long
+    std::thread keep_thr;
+    std::mutex keep_mu;
+    std::condition_variable keep_cv;
+    int32_t keep_us = 0;                // (under keep_mu) 0: off
+    bool keep_stop = false;             // (under keep_mu)
+    std::atomic<int64_t> last_use_ns{0};   // steady-clock time of the last call / batch start
+    hipStream_t keep_stream = nullptr;
+    unsigned* d_keep = nullptr;
+    int64_t keep_launches = 0;          // (the thread's own) kernels launched so far
 };
 
 namespace {
@@ -1090,7 +1103,16 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
 
 void mppi_destroy(mppi_engine* e) {
     if (!e) return;
+    if (e->keep_thr.joinable()) {   // the keep-alive thread first: it launches on this engine's device
+        {
+            std::lock_guard<std::mutex> lk(e->keep_mu);
+            e->keep_stop = true;
+        }
+        e->keep_cv.notify_all();
+        e->keep_thr.join();
+    }
     (void)hipSetDevice(e->cfg.device);
+    if (e->keep_stream) { (void)hipStreamSynchronize(e->keep_stream); (void)hipStreamDestroy(e->keep_stream); }
     // the native queue first: its last batch may still write the buffers freed below (stamps
     // included).  A queue that does not drain leaves them leaked rather than freed under it.
     if (e->aql && !mppi_aql::step_destroy(e->aql)) {
@@ -1115,7 +1137,7 @@ void mppi_destroy(mppi_engine* e) {
     for (void* q : e->x_opened) if (q) (void)hipIpcCloseMemHandle(q);
     void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_keep};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -1123,6 +1145,73 @@ void mppi_destroy(mppi_engine* e) {
     if (e->ev_out) (void)hipEventDestroy(e->ev_out);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
+}
+
+// ---------------------------------------------------------------- keep-alive (the node's idle gaps)
+namespace {
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Every keep_us: if no control call or batch started in the last keep_us, one k_keepalive on the
+// keep-alive stream (no wait for it).  Between ticks of a 100 Hz node the GPU, its queues and the
+// host link otherwise fall idle, and the next call pays for their wake-up.
+void keepalive_loop(mppi_engine* e) {
+    (void)hipSetDevice(e->cfg.device);
+    std::unique_lock<std::mutex> lk(e->keep_mu);
+    unsigned v = 0;
+    while (!e->keep_stop) {
+        const int32_t us = e->keep_us;
+        e->keep_cv.wait_for(lk, std::chrono::microseconds(us), [&] { return e->keep_stop || e->keep_us != us; });
+        if (e->keep_stop) break;
+        if (e->keep_us != us) continue;   // (the period changed: wait the new one)
+        if (steady_ns() - e->last_use_ns.load(std::memory_order_relaxed) < (int64_t)us * 1000) continue;
+        lk.unlock();
+        const bool ok = mppi_launch_keepalive(e->d_keep, ++v, e->keep_stream) == 0;
+        lk.lock();
+        if (ok) ++e->keep_launches;
+    }
+}
+}  // namespace
+
+mppi_status mppi_set_keepalive(mppi_engine* e, int32_t period_us) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (period_us != 0 && (period_us < 100 || period_us > 1000000))
+        return fail(MPPI_ERR_INVALID_ARG, "keep-alive period %d us: 0 (off) or 100 .. 1000000", period_us);
+    if (use_device(e)) return MPPI_ERR_HIP;
+    if (period_us > 0 && !e->d_keep) {
+        HIP_TRY(hipMalloc(&e->d_keep, 64));
+        HIP_TRY(hipStreamCreateWithFlags(&e->keep_stream, hipStreamNonBlocking));
+    }
+    if (period_us == 0) {
+        if (e->keep_thr.joinable()) {
+            {
+                std::lock_guard<std::mutex> lk(e->keep_mu);
+                e->keep_stop = true;
+                e->keep_us = 0;
+            }
+            e->keep_cv.notify_all();
+            e->keep_thr.join();
+            e->keep_stop = false;
+        }
+        return MPPI_OK;
+    }
+    {
+        std::lock_guard<std::mutex> lk(e->keep_mu);
+        e->keep_us = period_us;
+    }
+    e->keep_cv.notify_all();
+    if (!e->keep_thr.joinable()) e->keep_thr = std::thread(keepalive_loop, e);
+    return MPPI_OK;
+}
+
+mppi_status mppi_get_keepalive(mppi_engine* e, int32_t* period_us, int64_t* launches) {
+    if (!e || !period_us || !launches) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(e->keep_mu);
+    *period_us = e->keep_us;
+    *launches = e->keep_launches;
+    return MPPI_OK;
 }
 
 mppi_status mppi_set_stream(mppi_engine* e, void* s) {
@@ -1778,6 +1867,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out, float* u0,
                       mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (e->keep_thr.joinable()) e->last_use_ns.store(steady_ns(), std::memory_order_relaxed);
     if (sharded(e) && !e->comm)
         return fail(MPPI_ERR_STATE, "mppi_step on a shard needs mppi_comm_init (or use the split phases)");
     mppi_status st;
@@ -2025,6 +2115,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
 
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     if (!e || n < 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_run_steps: bad arguments");
+    if (e->keep_thr.joinable()) e->last_use_ns.store(steady_ns(), std::memory_order_relaxed);
     if (sharded(e) && !e->comm) return fail(MPPI_ERR_STATE, "mppi_run_steps on a shard needs mppi_comm_init");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_run_steps needs device noise");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_run_steps before mppi_set_state");

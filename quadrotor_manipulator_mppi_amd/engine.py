@@ -330,6 +330,17 @@ class Engine:
     def synchronize(self):
         capi.check(self._L.mppi_synchronize(self._h), "synchronize")
 
+    def set_keepalive(self, period_us: int):
+        """Keep the GPU out of its idle states between control ticks (mppi_set_keepalive): a tiny
+        kernel every ``period_us`` during which no step started; 0 turns it off."""
+        capi.check(self._L.mppi_set_keepalive(self._h, int(period_us)), "set_keepalive")
+
+    def keepalive(self):
+        """(period_us, kernels launched so far) of the keep-alive."""
+        us, n = C.c_int32(), C.c_int64()
+        capi.check(self._L.mppi_get_keepalive(self._h, C.byref(us), C.byref(n)), "get_keepalive")
+        return us.value, n.value
+
     def dispatch_info(self) -> str:
         """How the last run_steps / step were dispatched: "<aql | hip: why>; calls: <aql | hip>"."""
         buf = C.create_string_buffer(256)

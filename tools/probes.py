@@ -538,8 +538,14 @@ def probe_rate(model="arm", K="4096", H="32", calls="200"):
                                     ("spin 10 ms, touch /1ms", 0.01, True, 0.001, 0),
                                     ("spin 10 ms, touch -50us", 0.01, True, 0, 5e-5),
                                     ("sleep 10 ms, touch /1ms", 0.01, False, 0.001, 0),
+                                    ("sleep 10 ms, keepalive 1000", 0.01, False, 0, 1000),
+                                    ("sleep 10 ms, keepalive 200", 0.01, False, 0, 200),
+                                    ("sleep 10 ms, keepalive 100", 0.01, False, 0, 100),
                                     ("back-to-back (again)", 0.0, False, 0, 0)):
-        x = run(gap, spin, te, tb)
+        ka = tb if tb >= 100 else 0    # rows with an integer >= 100 there: the engine's keep-alive, us
+        e.set_keepalive(ka)
+        x = run(gap, spin, te, 0 if ka else tb)
+        e.set_keepalive(0)
         print(f"{model} K={K} H={H} {name:22s}: calls {x.size}  p50 {np.percentile(x, 50):6.1f} us  "
               f"p90 {np.percentile(x, 90):6.1f}  p99 {np.percentile(x, 99):6.1f}  mean {x.mean():6.1f}", flush=True)
     print(f"dispatch: {e.dispatch_info()}", flush=True)
