@@ -42,6 +42,7 @@ sys.path.insert(0, ROOT)
 HOME_Q = [1.57, 1.7, 0.0, 4.4, 0.0, 4.71, 0.0]                # kinova.py:135
 ARM_TARGET = ([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5])   # mppi.py:71-72
 DRONE_TARGET = [1.0, 2.0, 3.4]                                   # drone_mppi.py:141
+PREWARM_US = 200        # latency_100hz_prewarm's window (mppi_set_prewarm)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 C4_K_TOTAL = 65536      # BASELINE configs[3]: whole-body K=65536 H=64 over the node
 
@@ -419,11 +420,12 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
             lat.append(time.perf_counter() - t1)
     eng.synchronize()
     lat100 = latency_at_rate(se, state, lat_rate_calls) if lat_rate_calls else []
-    lat100k = []
-    if lat_rate_calls:   # the same cadence with the engine's keep-alive on (mppi_set_keepalive, 1 ms)
-        eng.set_keepalive(1000)
-        lat100k = latency_at_rate(se, state, lat_rate_calls)
-        eng.set_keepalive(0)
+    lat100p, pw_touches = [], 0
+    if lat_rate_calls:   # the same cadence with the engine's prewarm on (mppi_set_prewarm)
+        eng.set_prewarm(PREWARM_US)
+        lat100p = latency_at_rate(se, state, lat_rate_calls)
+        pw_touches = eng.prewarm()[1]
+        eng.set_prewarm(0)
     if not lat and not lat100:
         se.step(state)
     dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
@@ -432,7 +434,7 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.mode == "rccl" else None
     res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
-           "lat100_keepalive": lat100k,
+           "lat100_prewarm": lat100p, "prewarm_touches": pw_touches,
            "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
            "K": eng.K, "H": eng.H,
            "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
@@ -542,7 +544,8 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
         "latency_p50_ms": float(np.median(lat)) if lat.size else None,
         "latency_p99_ms": float(np.percentile(lat, 99)) if lat.size else None,
         "latency_100hz": latency_100hz(r.get("lat100"), lat),
-        "latency_100hz_keepalive": latency_100hz(r.get("lat100_keepalive"), lat, keepalive_us=1000),
+        "latency_100hz_prewarm": latency_100hz(r.get("lat100_prewarm"), lat, prewarm_us=PREWARM_US,
+                                               touches=r.get("prewarm_touches")),
         "kernels": {k: v for k, v in tim.items() if k != "rollout_us_batches"} if tim is not None else None,
         "roofline": rf,
         "cpu_baseline": cpu,
@@ -571,9 +574,9 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
     return line
 
 
-def latency_100hz(lat100, lat_b2b, keepalive_us=0):
+def latency_100hz(lat100, lat_b2b, prewarm_us=0, touches=None):
     """The control call at the node's 100 Hz cadence (latency_at_rate) beside the back-to-back one;
-    with ``keepalive_us`` the engine's keep-alive (mppi_set_keepalive) ran during the idle gaps."""
+    with ``prewarm_us`` the engine's prewarm (mppi_set_prewarm) ran with that window."""
     if not lat100:
         return None
     x = np.array(lat100) * 1e3
@@ -582,11 +585,14 @@ def latency_100hz(lat100, lat_b2b, keepalive_us=0):
     what = ("host-inclusive control call (state in, outputs, check_reach) started on every 10 ms tick after "
             "100 ms idle, no heat-up: the arm node's rospy.Rate(100) loop (kinova.py:101); the GPU idles "
             "~10 ms between calls")
-    if keepalive_us:
-        what += f"; the engine's keep-alive on: a one-wave kernel every {keepalive_us} us of idle (mppi_set_keepalive)"
-    return {"p50_ms": p50, "p99_ms": float(np.percentile(x, 99)), "mean_ms": float(x.mean()), "calls": int(x.size),
-            "period_ms": 10.0, "vs_back_to_back_p50": p50 / b2b if b2b else None, "keepalive_us": keepalive_us,
-            "what": what}
+    r = {"p50_ms": p50, "p99_ms": float(np.percentile(x, 99)), "mean_ms": float(x.mean()), "calls": int(x.size),
+         "period_ms": 10.0, "vs_back_to_back_p50": p50 / b2b if b2b else None}
+    if prewarm_us:
+        what += (f"; the engine's prewarm on (mppi_set_prewarm, window {prewarm_us} us): its native queue touched "
+                 "every 25 us from the window's start until the predicted call")
+        r.update(prewarm_us=prewarm_us, prewarm_touches=touches)
+    r["what"] = what
+    return r
 
 
 def secondary_entry(s, ns):

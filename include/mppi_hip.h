@@ -346,16 +346,19 @@ mppi_status mppi_dispatch_info(mppi_engine* e, char* buf, int32_t len);
 
 mppi_status mppi_synchronize(mppi_engine* e);
 
-/* Keep-alive for a controller that ticks with idle gaps (the arm node's rospy.Rate(100) loop,
- * kinova.py:101; no reference counterpart -- the reference's torch calls pay the same wake-up): while
- * period_us > 0, a host thread of the engine launches a one-wave kernel on its own stream every
- * period_us during which no mppi_step / mppi_run_steps started, so the GPU, its queues and the
- * host link stay out of their idle states between ticks.  It touches no engine state (results are
- * unchanged) and costs one tiny kernel per period.  period_us: 0 = off (the default), else
- * 100 .. 1000000.  mppi_destroy stops it.  mppi_get_keepalive: the period and the kernels
- * launched so far. */
-mppi_status mppi_set_keepalive(mppi_engine* e, int32_t period_us);
-mppi_status mppi_get_keepalive(mppi_engine* e, int32_t* period_us, int64_t* launches);
+/* Prewarm for a controller that ticks with idle gaps (the arm node's rospy.Rate(100) loop,
+ * kinova.py:101; no reference counterpart -- the reference's torch calls pay the same wake-up).
+ * A call on a native queue left idle for more than ~50-100 us runs ~6-7 us longer than back to
+ * back.  While window_us > 0 a host thread of the engine predicts the next mppi_step from the
+ * median interval of the last calls' start times and, from window_us before that until the call
+ * starts (at most window_us after it), puts a pair of one-wave packets on the engine's native
+ * queue every 25 us; those write a scratch word only, so results are unchanged.  Calls back to back
+ * (interval < 4 windows) or slower than 1 s get no touches; with HIP dispatch (no native queue)
+ * it does nothing.  The thread spins through each window (2 x window_us of one core per tick).
+ * window_us: 0 = off (the default), else 50 .. 5000.  mppi_destroy stops it.
+ * mppi_get_prewarm: the window and the touches so far. */
+mppi_status mppi_set_prewarm(mppi_engine* e, int32_t window_us);
+mppi_status mppi_get_prewarm(mppi_engine* e, int32_t* window_us, int64_t* touches);
 
 /* Readback in the reference's layouts (synchronous):
  *   costs    S (V,K)                         compute_all_cost()

@@ -117,8 +117,8 @@ PROTOTYPES = {
     "mppi_run_steps": (_ST, [_P, C.c_int32]),
     "mppi_dispatch_info": (_ST, [_P, C.c_char_p, C.c_int32]),
     "mppi_synchronize": (_ST, [_P]),
-    "mppi_set_keepalive": (_ST, [_P, C.c_int32]),
-    "mppi_get_keepalive": (_ST, [_P, _I32, C.POINTER(C.c_int64)]),
+    "mppi_set_prewarm": (_ST, [_P, C.c_int32]),
+    "mppi_get_prewarm": (_ST, [_P, _I32, C.POINTER(C.c_int64)]),
     "mppi_get_costs": (_ST, [_P, _F]),
     "mppi_get_weights": (_ST, [_P, _F]),
     "mppi_get_noise": (_ST, [_P, _F]),

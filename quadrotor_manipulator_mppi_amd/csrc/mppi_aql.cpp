@@ -261,6 +261,12 @@ struct Step {
     uint32_t step_off = 0, step_word = 0; // the resident rollout's dispatch-id relative step word
     bool valid = false;
     int64_t outstanding = 0;              // batches dispatched and not yet waited for
+    unsigned char* d_touch = nullptr;     // step_touch: two 64 B argument blocks, then its 16 B output
+    Kern kt;
+    // the queue is single-producer: every function below that writes packets or waits holds this
+    // (recursive: step_call and step_prepare wait inside), so the engine's prewarm thread
+    // (step_touch) and the control calls never write packets at the same time
+    std::recursive_mutex mu;
 };
 
 void set_capture(mppi::LaunchDesc* d) { t_capture = d; }
@@ -332,12 +338,17 @@ bool step_destroy(Step* s) {
     hsa_signal_destroy(s->done);
     hsa_queue_destroy(s->q);
     (void)hipFree(s->d_args);
+    if (s->d_touch) (void)hipFree(s->d_touch);
     if (s->call_vis) hsa_amd_memory_pool_free(s->h_call); else (void)hipHostFree(s->h_call);
     delete s;
     return true;
 }
 
-bool step_busy(Step* s) { return s && s->outstanding > 0; }
+bool step_busy(Step* s) {
+    if (!s) return false;
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
+    return s->outstanding > 0;
+}
 
 // a launch's argument block against the kernel's: only explicit arguments (no hidden ones),
 // LDS within the CU's 160 KB.  (Scratch: the packet carries the kernel's private segment size;
@@ -368,6 +379,7 @@ static unsigned char* batch_args(Step* s) { return s->d_args + (1 + 2 * (size_t)
 
 int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
                  uint32_t step_off, std::string* err) {
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
     // the next rollout's packet index (the queue holds (rollout, finalize) pairs only, so
     // rollouts sit at indices of one parity and (index >> 1) counts pairs)
     const uint32_t word = step - (uint32_t)(hsa_queue_load_write_index_relaxed(s->q) >> 1);
@@ -534,6 +546,7 @@ static bool probe_dispatch_ids(Step* s, std::string* why) {
 }
 
 int step_dispatch(Step* s, int n, std::string* err) {
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
     if (!s->valid) { *err = "step_dispatch before step_prepare"; return -1; }
     if (n <= 0) return 0;
     if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
@@ -555,6 +568,7 @@ int step_dispatch(Step* s, int n, std::string* err) {
 
 int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin, uint32_t step,
               uint32_t step_off, uint32_t seq_off, uint32_t* seq, std::string* err) {
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
     if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
     static const bool prof = getenv("MPPI_AQL_PROFILE") != nullptr;   // diagnostics: phases of a call
     static double pacc[4] = {0, 0, 0, 0};
@@ -632,6 +646,44 @@ int step_call(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& fin
     return 0;
 }
 
+int step_touch(Step* s, bool if_free, std::string* err) {
+    std::unique_lock<std::recursive_mutex> qlk(s->mu, std::defer_lock);
+    if (if_free) {
+        if (!qlk.try_lock()) return 1;
+    } else {
+        qlk.lock();
+    }
+    if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
+    if (!s->d_touch) {
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            if (!lookup(s->dev, "k_dispatch_probe", &s->kt, err)) return -2;
+        }
+        if (hipMalloc(&s->d_touch, 3 * 64) != hipSuccess) { *err = "touch buffer"; s->d_touch = nullptr; return -1; }
+        unsigned char h[128] = {};
+        unsigned char* outs[2] = {s->d_touch + 128, s->d_touch + 136};
+        memcpy(h, &outs[0], 8);
+        memcpy(h + 64, &outs[1], 8);
+        if (hipMemcpy(s->d_touch, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) { *err = "touch upload"; return -1; }
+    }
+    mppi::LaunchDesc l{};
+    l.grid[0] = l.grid[1] = l.grid[2] = 1;
+    l.block[0] = 64; l.block[1] = l.block[2] = 1;
+    l.arg_bytes = 8;
+    // a pair, so rollouts keep their packet-index parity; the next batch re-uploads its step word
+    hsa_signal_add_relaxed(s->done, 1);
+    ++s->outstanding;
+    put(s->q, s->kt, l, s->d_touch, hsa_signal_t{0}, 1, 0);
+    put(s->q, s->kt, l, s->d_touch + 64, s->done, 0, 0);
+    hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);
+    return 0;
+}
+
+void step_ring(Step* s) {
+    const uint64_t w = hsa_queue_load_write_index_relaxed(s->q);
+    if (w) hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)(w - 1));
+}
+
 int step_error(Step* s) { return s ? s->qerr.load() : 0; }
 
 const char* step_call_memory(Step* s) {
@@ -639,11 +691,15 @@ const char* step_call_memory(Step* s) {
 }
 
 void step_call_read(Step* s) {
-    if (s) s->call_unread = false;
+    if (!s) return;
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
+    s->call_unread = false;
 }
 
 int step_wait(Step* s, int timeout_ms, std::string* err) {
-    if (!s || !s->outstanding) return 0;
+    if (!s) return 0;
+    std::lock_guard<std::recursive_mutex> qlk(s->mu);
+    if (!s->outstanding) return 0;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         if (hsa_signal_load_scacquire(s->done) == 0) break;

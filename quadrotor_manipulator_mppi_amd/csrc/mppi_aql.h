@@ -53,6 +53,15 @@ void step_call_read(Step* s);
 // fine-grained", "device coarse-grained": written by the host through the BAR; or "pinned host
 // memory", read over PCIe by every block: MPPI_AQL_CALL_HOSTMEM=1 or no host-writable pool).
 const char* step_call_memory(Step* s);
+// Two one-wave packets (k_dispatch_probe into a scratch word) on the engine's queue: its
+// packet processor and queue state exercised, no engine buffer touched (the next batch re-uploads
+// its step word: the pair moved the packet indices).  From any thread.  if_free: 1 without
+// touching when another thread holds the queue.  0 / 1 / -2 / -1.
+int step_touch(Step* s, bool if_free, std::string* err);
+// The doorbell rung again with the last packet's index: no packet, nothing dispatched.
+// Only from the thread that writes the packets (a stale index rung after a newer one would hide
+// the newer packets from the packet processor).
+void step_ring(Step* s);
 // The queue's asynchronous error, if any (0 = none).
 int step_error(Step* s);
 // Until every dispatched pair has completed.  -1 on a queue error or after timeout_ms.

@@ -8,6 +8,7 @@
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -415,17 +416,17 @@ struct mppi_engine {
     bool aql_call = false;              // ... from a native control call (flags carry bit 31)
     bool calls_native = false;          // the last mppi_step went out as native packets
     double call_wait_us = 0.0;          // diagnostics (MPPI_AQL_PROFILE): the last call's flag wait
-    // keep-alive (mppi_set_keepalive): a host thread launches k_keepalive on its own stream every
-    // keep_us while no control call or batch has started for that long
-    std::thread keep_thr;
-    std::mutex keep_mu;
-    std::condition_variable keep_cv;
-    int32_t keep_us = 0;                // (under keep_mu) 0: off
-    bool keep_stop = false;             // (under keep_mu)
-    std::atomic<int64_t> last_use_ns{0};   // steady-clock time of the last call / batch start
-    hipStream_t keep_stream = nullptr;
-    unsigned* d_keep = nullptr;
-    int64_t keep_launches = 0;          // (the thread's own) kernels launched so far
+    // prewarm (mppi_set_prewarm): a host thread learns the control calls' cadence from their start
+    // times and touches the native queue through a window before each predicted call
+    std::thread pw_thr;
+    std::mutex pw_mu;                   // (for pw_cv only)
+    std::condition_variable pw_cv;
+    std::atomic<int32_t> pw_us{0};      // the window half-width; 0: off
+    std::atomic<bool> pw_stop{false};
+    std::atomic<int64_t> pw_touches{0};
+    std::atomic<int64_t> call_t[8];     // steady-clock start of the last 8 control calls (ring)
+    std::atomic<int64_t> call_n{0};     // control calls recorded
+    bool pw_spin = false;               // diagnostics (MPPI_PREWARM_SPIN=1): spin between touches
 };
 
 namespace {
@@ -1101,18 +1102,12 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     return MPPI_OK;
 }
 
+namespace { void prewarm_stop(mppi_engine* e); }
+
 void mppi_destroy(mppi_engine* e) {
     if (!e) return;
-    if (e->keep_thr.joinable()) {   // the keep-alive thread first: it launches on this engine's device
-        {
-            std::lock_guard<std::mutex> lk(e->keep_mu);
-            e->keep_stop = true;
-        }
-        e->keep_cv.notify_all();
-        e->keep_thr.join();
-    }
+    prewarm_stop(e);   // the prewarm thread first: it writes packets into the native queue
     (void)hipSetDevice(e->cfg.device);
-    if (e->keep_stream) { (void)hipStreamSynchronize(e->keep_stream); (void)hipStreamDestroy(e->keep_stream); }
     // the native queue first: its last batch may still write the buffers freed below (stamps
     // included).  A queue that does not drain leaves them leaked rather than freed under it.
     if (e->aql && !mppi_aql::step_destroy(e->aql)) {
@@ -1137,7 +1132,7 @@ void mppi_destroy(mppi_engine* e) {
     for (void* q : e->x_opened) if (q) (void)hipIpcCloseMemHandle(q);
     void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_keep};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);
@@ -1147,70 +1142,94 @@ void mppi_destroy(mppi_engine* e) {
     delete e;
 }
 
-// ---------------------------------------------------------------- keep-alive (the node's idle gaps)
+// ---------------------------------------------------------------- prewarm (the node's idle gaps)
+// At the node's cadence (rospy.Rate(100), kinova.py:101) the engine's queue sits empty ~10 ms
+// between calls, and a call on a queue idle for more than ~50-100 us runs ~6-7 us longer than
+// back to back; a pair of one-wave packets on the same queue 20-50 us before the call removes
+// that, a touch 100 us or more before it does not, nor does a touch on another queue or the
+// doorbell alone (profiles/r05/prewarm/).  So the thread predicts the next call from the median
+// interval of the last calls and, from pw_us before the prediction until the call starts (or
+// pw_us after it), touches the queue every kTouchNs.  Calls back to back or slower than 1 s get
+// no touches; nothing the engine computes changes (the touch writes a scratch word only).
 namespace {
+constexpr int64_t kTouchNs = 25000;
+
 int64_t steady_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
 }
 
-// Every keep_us: if no control call or batch started in the last keep_us, one k_keepalive on the
-// keep-alive stream (no wait for it).  Between ticks of a 100 Hz node the GPU, its queues and the
-// host link otherwise fall idle, and the next call pays for their wake-up.
-void keepalive_loop(mppi_engine* e) {
-    (void)hipSetDevice(e->cfg.device);
-    std::unique_lock<std::mutex> lk(e->keep_mu);
-    unsigned v = 0;
-    while (!e->keep_stop) {
-        const int32_t us = e->keep_us;
-        e->keep_cv.wait_for(lk, std::chrono::microseconds(us), [&] { return e->keep_stop || e->keep_us != us; });
-        if (e->keep_stop) break;
-        if (e->keep_us != us) continue;   // (the period changed: wait the new one)
-        if (steady_ns() - e->last_use_ns.load(std::memory_order_relaxed) < (int64_t)us * 1000) continue;
-        lk.unlock();
-        const bool ok = mppi_launch_keepalive(e->d_keep, ++v, e->keep_stream) == 0;
+void note_call(mppi_engine* e) {   // mppi_step entry (the caller's thread)
+    if (!e->pw_us.load(std::memory_order_relaxed)) return;
+    const int64_t n = e->call_n.load(std::memory_order_relaxed);
+    e->call_t[n % 8].store(steady_ns(), std::memory_order_relaxed);
+    e->call_n.store(n + 1, std::memory_order_release);
+}
+
+void prewarm_loop(mppi_engine* e) {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);   // this thread's sleeps end ~1 us after their deadline
+    std::unique_lock<std::mutex> lk(e->pw_mu);
+    auto nap = [&](int64_t ns) { e->pw_cv.wait_for(lk, std::chrono::nanoseconds(ns), [&] { return e->pw_stop.load(); }); };
+    while (!e->pw_stop.load()) {
+        const int64_t win = (int64_t)e->pw_us.load() * 1000;
+        const int64_t n = e->call_n.load(std::memory_order_acquire);
+        if (n < 4 || !e->aql) { nap(2000000); continue; }   // (e->aql is set before the first recorded call ends)
+        const int m = (int)std::min<int64_t>(n, 8);
+        int64_t t[8], d[8];
+        for (int i = 0; i < m; ++i) t[i] = e->call_t[(n - m + i) % 8].load(std::memory_order_relaxed);
+        for (int i = 1; i < m; ++i) d[i - 1] = t[i] - t[i - 1];
+        std::nth_element(d, d + (m - 1) / 2, d + (m - 1));
+        const int64_t P = d[(m - 1) / 2], last = t[m - 1];
+        const int64_t start = last + P - win, end = last + P + win, now = steady_ns();
+        if (P < 4 * win || P > 1000000000 || now > end) { nap(2000000); continue; }   // no cadence, or the call is late
+        if (now < start - 200000) { nap(start - 100000 - now); continue; }           // (then look again)
+        lk.unlock();   // through the window: a touch, then sleep to the next (the host keeps its core)
+        int64_t next = start;
+        while (!e->pw_stop.load(std::memory_order_relaxed) && e->call_n.load(std::memory_order_acquire) == n) {
+            const int64_t tn = steady_ns();
+            if (tn > end) break;
+            if (tn >= next) {
+                std::string err;
+                if (mppi_aql::step_touch(e->aql, true, &err) == 0) e->pw_touches.fetch_add(1, std::memory_order_relaxed);
+                next = tn + kTouchNs;
+            }
+            if (e->pw_spin) _mm_pause();
+            else std::this_thread::sleep_for(std::chrono::nanoseconds(std::max<int64_t>(1000, next - steady_ns())));
+        }
         lk.lock();
-        if (ok) ++e->keep_launches;
+        if (e->call_n.load(std::memory_order_acquire) == n) nap(1000000);   // the window passed without the call
     }
+}
+
+void prewarm_stop(mppi_engine* e) {
+    if (!e->pw_thr.joinable()) return;
+    {
+        std::lock_guard<std::mutex> lk(e->pw_mu);
+        e->pw_stop.store(true);
+    }
+    e->pw_cv.notify_all();
+    e->pw_thr.join();
+    e->pw_stop.store(false);
 }
 }  // namespace
 
-mppi_status mppi_set_keepalive(mppi_engine* e, int32_t period_us) {
+mppi_status mppi_set_prewarm(mppi_engine* e, int32_t window_us) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
-    if (period_us != 0 && (period_us < 100 || period_us > 1000000))
-        return fail(MPPI_ERR_INVALID_ARG, "keep-alive period %d us: 0 (off) or 100 .. 1000000", period_us);
-    if (use_device(e)) return MPPI_ERR_HIP;
-    if (period_us > 0 && !e->d_keep) {
-        HIP_TRY(hipMalloc(&e->d_keep, 64));
-        HIP_TRY(hipStreamCreateWithFlags(&e->keep_stream, hipStreamNonBlocking));
-    }
-    if (period_us == 0) {
-        if (e->keep_thr.joinable()) {
-            {
-                std::lock_guard<std::mutex> lk(e->keep_mu);
-                e->keep_stop = true;
-                e->keep_us = 0;
-            }
-            e->keep_cv.notify_all();
-            e->keep_thr.join();
-            e->keep_stop = false;
-        }
-        return MPPI_OK;
-    }
-    {
-        std::lock_guard<std::mutex> lk(e->keep_mu);
-        e->keep_us = period_us;
-    }
-    e->keep_cv.notify_all();
-    if (!e->keep_thr.joinable()) e->keep_thr = std::thread(keepalive_loop, e);
+    if (window_us != 0 && (window_us < 50 || window_us > 5000))
+        return fail(MPPI_ERR_INVALID_ARG, "prewarm window %d us: 0 (off) or 50 .. 5000", window_us);
+    prewarm_stop(e);
+    e->pw_us.store(window_us);
+    e->call_n.store(0);
+    const char* spin = getenv("MPPI_PREWARM_SPIN");
+    e->pw_spin = spin && spin[0] == '1';
+    if (window_us) e->pw_thr = std::thread(prewarm_loop, e);
     return MPPI_OK;
 }
 
-mppi_status mppi_get_keepalive(mppi_engine* e, int32_t* period_us, int64_t* launches) {
-    if (!e || !period_us || !launches) return fail(MPPI_ERR_INVALID_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(e->keep_mu);
-    *period_us = e->keep_us;
-    *launches = e->keep_launches;
+mppi_status mppi_get_prewarm(mppi_engine* e, int32_t* window_us, int64_t* touches) {
+    if (!e || !window_us || !touches) return fail(MPPI_ERR_INVALID_ARG, "null argument");
+    *window_us = e->pw_us.load();
+    *touches = e->pw_touches.load();
     return MPPI_OK;
 }
 
@@ -1867,7 +1886,7 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
 mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise, double* out, float* u0,
                       mppi_stats* stats) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
-    if (e->keep_thr.joinable()) e->last_use_ns.store(steady_ns(), std::memory_order_relaxed);
+    note_call(e);
     if (sharded(e) && !e->comm)
         return fail(MPPI_ERR_STATE, "mppi_step on a shard needs mppi_comm_init (or use the split phases)");
     mppi_status st;
@@ -2115,7 +2134,6 @@ static mppi_status control_call_aql(mppi_engine* e, const double* state, bool* u
 
 mppi_status mppi_run_steps(mppi_engine* e, int32_t n) {
     if (!e || n < 0) return fail(MPPI_ERR_INVALID_ARG, "mppi_run_steps: bad arguments");
-    if (e->keep_thr.joinable()) e->last_use_ns.store(steady_ns(), std::memory_order_relaxed);
     if (sharded(e) && !e->comm) return fail(MPPI_ERR_STATE, "mppi_run_steps on a shard needs mppi_comm_init");
     if (e->cfg.noise_mode != MPPI_NOISE_PHILOX) return fail(MPPI_ERR_STATE, "mppi_run_steps needs device noise");
     if (!e->state_set) return fail(MPPI_ERR_STATE, "mppi_run_steps before mppi_set_state");
@@ -2420,6 +2438,22 @@ int64_t mppi_debug_fstamps(mppi_engine* e, unsigned long long* out, int64_t max_
             hipSuccess)
         return MPPI_ERR_HIP;
     return n;
+}
+
+// Diagnostic (not part of the public header): mppi_aql step_touch on the engine's own queue
+// (tools/probes.py rate_split).  Same thread as the control calls.
+int32_t mppi_debug_queue_touch(mppi_engine* e) {
+    if (!e || !e->aql) return MPPI_ERR_INVALID_ARG;
+    std::string err;
+    const int r = mppi_aql::step_touch(e->aql, false, &err);
+    return r == 0 ? MPPI_OK : fail(MPPI_ERR_HIP, "queue touch: %s", err.c_str());
+}
+
+// Diagnostic: mppi_aql step_ring (the doorbell again, no packet).
+int32_t mppi_debug_queue_ring(mppi_engine* e) {
+    if (!e || !e->aql) return MPPI_ERR_INVALID_ARG;
+    mppi_aql::step_ring(e->aql);
+    return MPPI_OK;
 }
 
 int32_t mppi_philox_words(int32_t A) {

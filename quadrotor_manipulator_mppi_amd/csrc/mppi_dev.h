@@ -257,7 +257,6 @@ int mppi_launch_rollout_arm32(const mppi::DevParams* p, int block_threads, void*
 int mppi_launch_rollout_wb(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_rollout_quad(const mppi::DevParams* p, int block_threads, void* stream);
 int mppi_launch_finalize(const mppi::FinParams* p, void* stream);
-int mppi_launch_keepalive(unsigned* word, unsigned v, void* stream);
 int mppi_launch_peer_probe(unsigned long long* const* peers, unsigned long long* local, int n, int me,
                            unsigned long long slot_words, uint32_t tag, unsigned long long ticks,
                            unsigned long long* out, void* stream);

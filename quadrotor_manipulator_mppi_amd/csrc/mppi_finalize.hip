@@ -601,18 +601,6 @@ extern "C" int mppi_launch_peer_probe(unsigned long long* const* peers, unsigned
     return (int)hipGetLastError();
 }
 
-// Keep-alive (mppi_set_keepalive): one wave that stores one word, launched on its own stream
-// every period while the controller idles between ticks, so the GPU, its queues and the host link
-// stay out of their idle states (profiles/r05/rate_probe_touch.txt).  Touches no engine state.
-__global__ void __launch_bounds__(64) k_keepalive(unsigned* word, unsigned v) {
-    if (threadIdx.x == 0) word[0] = v;
-}
-
-extern "C" int mppi_launch_keepalive(unsigned* word, unsigned v, void* stream) {
-    hipLaunchKernelGGL(k_keepalive, dim3(1), dim3(64), 0, (hipStream_t)stream, word, v);
-    return (int)hipGetLastError();
-}
-
 // w_k = exp(-(S_k - rho)/lambda) / eta  (mppi.py:184-191) -- readback only
 __global__ void k_weights(const float* S, const float* stats, float* w, int V, int K, float coef) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -330,15 +330,15 @@ class Engine:
     def synchronize(self):
         capi.check(self._L.mppi_synchronize(self._h), "synchronize")
 
-    def set_keepalive(self, period_us: int):
-        """Keep the GPU out of its idle states between control ticks (mppi_set_keepalive): a tiny
-        kernel every ``period_us`` during which no step started; 0 turns it off."""
-        capi.check(self._L.mppi_set_keepalive(self._h, int(period_us)), "set_keepalive")
+    def set_prewarm(self, window_us: int):
+        """Warm the native queue before each predicted control call (mppi_set_prewarm): for a node
+        that ticks with idle gaps (100 Hz).  ``window_us`` 50 .. 5000; 0 turns it off."""
+        capi.check(self._L.mppi_set_prewarm(self._h, int(window_us)), "set_prewarm")
 
-    def keepalive(self):
-        """(period_us, kernels launched so far) of the keep-alive."""
+    def prewarm(self):
+        """(window_us, queue touches so far) of the prewarm."""
         us, n = C.c_int32(), C.c_int64()
-        capi.check(self._L.mppi_get_keepalive(self._h, C.byref(us), C.byref(n)), "get_keepalive")
+        capi.check(self._L.mppi_get_prewarm(self._h, C.byref(us), C.byref(n)), "get_prewarm")
         return us.value, n.value
 
     def dispatch_info(self) -> str:

@@ -538,17 +538,143 @@ def probe_rate(model="arm", K="4096", H="32", calls="200"):
                                     ("spin 10 ms, touch /1ms", 0.01, True, 0.001, 0),
                                     ("spin 10 ms, touch -50us", 0.01, True, 0, 5e-5),
                                     ("sleep 10 ms, touch /1ms", 0.01, False, 0.001, 0),
-                                    ("sleep 10 ms, keepalive 1000", 0.01, False, 0, 1000),
-                                    ("sleep 10 ms, keepalive 200", 0.01, False, 0, 200),
-                                    ("sleep 10 ms, keepalive 100", 0.01, False, 0, 100),
+                                    ("sleep 10 ms, prewarm 100", 0.01, False, 0, 100),
+                                    ("sleep 10 ms, prewarm 200", 0.01, False, 0, 200),
+                                    ("sleep 10 ms, prewarm 500", 0.01, False, 0, 500),
+                                    ("spin 10 ms, prewarm 200", 0.01, True, 0, 200),
                                     ("back-to-back (again)", 0.0, False, 0, 0)):
-        ka = tb if tb >= 100 else 0    # rows with an integer >= 100 there: the engine's keep-alive, us
-        e.set_keepalive(ka)
-        x = run(gap, spin, te, 0 if ka else tb)
-        e.set_keepalive(0)
+        pw = tb if tb >= 50 else 0    # rows with an integer >= 50 there: the engine's prewarm window, us
+        e.set_prewarm(pw)
+        x = run(gap, spin, te, 0 if pw else tb)
+        e.set_prewarm(0)
         print(f"{model} K={K} H={H} {name:22s}: calls {x.size}  p50 {np.percentile(x, 50):6.1f} us  "
               f"p90 {np.percentile(x, 90):6.1f}  p99 {np.percentile(x, 99):6.1f}  mean {x.mean():6.1f}", flush=True)
     print(f"dispatch: {e.dispatch_info()}", flush=True)
+    e.close()
+
+
+def probe_rate_split(model="arm", K="4096", H="32", calls="200"):
+    """Where the ~7 us between a spin-gap call and a back-to-back call goes (probe_rate: the host
+    thread stays awake, only the device side idles 10 ms).  Every row spins 10 ms, then before the
+    timed call does one of: nothing; a torch kernel on another stream 5 us before; torch kernels
+    every 20 us through the gap; a control call on a second engine (its own AQL queue, same kernels)
+    50 us / 5 us before; a control call on the same engine 50 us before (its own queue warm, the
+    call's outputs and arguments just touched).  Rows that recover back-to-back latency name the
+    state that went cold."""
+    K, H, n = int(K), int(H), int(calls)
+    state = np.array(STATES[model], np.float64)
+    e, e2 = _engine(model, K, H), _engine(model, K, H)
+    for _ in range(100):
+        e.step(state)
+        e2.step(state)
+
+    import torch
+    buf = torch.zeros(16, device="cuda:0")
+    side = torch.cuda.Stream(device=0)
+
+    def torch_touch():
+        with torch.cuda.stream(side):
+            buf.add_(1.0)
+
+    L = e._L
+    L.mppi_debug_queue_touch.restype = C.c_int32
+    L.mppi_debug_queue_touch.argtypes = [C.c_void_p]
+
+    L.mppi_debug_queue_ring.restype = C.c_int32
+    L.mppi_debug_queue_ring.argtypes = [C.c_void_p]
+
+    def qring():    # the doorbell again with the last packet's index (mppi_aql step_ring)
+        assert L.mppi_debug_queue_ring(e._h) == 0
+
+    def qtouch():   # two one-wave packets on the engine's own AQL queue (mppi_aql step_touch)
+        assert L.mppi_debug_queue_touch(e._h) == 0
+
+    def spin(t_end, every=0.0, fn=None):
+        t_next = time.perf_counter()
+        while time.perf_counter() < t_end:
+            if every and time.perf_counter() >= t_next:
+                fn()
+                t_next += every
+
+    def run(before_s=0.0, fn=None, every=0.0):
+        lat = []
+        for _ in range(n):
+            t_end = time.perf_counter() + 0.01
+            if every:
+                spin(t_end, every, fn)
+            else:
+                spin(t_end - before_s)
+                if fn:
+                    fn()
+                spin(t_end)
+            t0 = time.perf_counter()
+            e.step(state)
+            lat.append(time.perf_counter() - t0)
+        return np.array(lat) * 1e6
+
+    rows = (("back-to-back", None),
+            ("spin 10 ms", dict()),
+            ("spin, torch touch -5us", dict(before_s=5e-6, fn=torch_touch)),
+            ("spin, torch touch /20us", dict(every=2e-5, fn=torch_touch)),
+            ("spin, engine2 call -50us", dict(before_s=5e-5, fn=lambda: e2.step(state))),
+            ("spin, engine2 call -5us", dict(before_s=5e-6, fn=lambda: e2.step(state))),
+            ("spin, same-engine call -50us", dict(before_s=5e-5, fn=lambda: e.step(state))),
+            ("spin, queue touch -20us", dict(before_s=2e-5, fn=qtouch)),
+            ("spin, queue touch -50us", dict(before_s=5e-5, fn=qtouch)),
+            ("spin, queue touch -100us", dict(before_s=1e-4, fn=qtouch)),
+            ("spin, queue touch -200us", dict(before_s=2e-4, fn=qtouch)),
+            ("spin, queue touch -300us", dict(before_s=3e-4, fn=qtouch)),
+            ("spin, queue touch -500us", dict(before_s=5e-4, fn=qtouch)),
+            ("spin, queue touch -0us", dict(before_s=1e-9, fn=qtouch)),
+            ("spin, doorbell -50us", dict(before_s=5e-5, fn=qring)),
+            ("spin, doorbell -20us", dict(before_s=2e-5, fn=qring)),
+            ("spin, doorbell -5us", dict(before_s=5e-6, fn=qring)),
+            ("spin, doorbell -0us", dict(before_s=1e-9, fn=qring)),
+            ("spin, queue touch /1ms", dict(every=1e-3, fn=qtouch)),
+            ("back-to-back (again)", None))
+    for name, kw in rows:
+        if kw is None:
+            lat = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                e.step(state)
+                lat.append(time.perf_counter() - t0)
+            x = np.array(lat) * 1e6
+        else:
+            x = run(**kw)
+        print(f"{model} K={K} H={H} {name:30s}: calls {x.size}  p50 {np.percentile(x, 50):6.1f} us  "
+              f"p90 {np.percentile(x, 90):6.1f}  p99 {np.percentile(x, 99):6.1f}  mean {x.mean():6.1f}", flush=True)
+    e2.close()
+    e.close()
+
+
+def probe_rate_prewarm(model="arm", K="4096", H="32", calls="200", rounds="3", windows="200"):
+    """bench.py's 100 Hz loop (latency_at_rate) with the prewarm off and on (mppi_set_prewarm),
+    alternating blocks of `calls` for `rounds` rounds per window, so that box noise falls on both:
+    per block p50/p90/p99/max, then the pooled percentiles per setting and the touches per call."""
+    import bench
+    K, H, n, R = int(K), int(H), int(calls), int(rounds)
+    state = np.array(STATES[model], np.float64)
+    e = _engine(model, K, H)
+    for _ in range(100):
+        e.step(state)
+    wins = [w for w in windows.split(",")]   # "200" sleep between touches, "200s" spin through the window
+    pooled = {w: [] for w in ["0"] + wins}
+    for r in range(R):
+        for w in ["0"] + wins:
+            os.environ["MPPI_PREWARM_SPIN"] = "1" if w.endswith("s") else "0"
+            e.set_prewarm(int(w.rstrip("s")))
+            t0 = e.prewarm()[1]
+            x = np.array(bench.latency_at_rate(e, state, n, idle_s=0.02)) * 1e6
+            t1 = e.prewarm()[1]
+            e.set_prewarm(0)
+            pooled[w].append(x)
+            print(f"round {r} prewarm {w:>5s}: p50 {np.percentile(x, 50):6.1f} us  p90 {np.percentile(x, 90):6.1f}  "
+                  f"p99 {np.percentile(x, 99):6.1f}  max {x.max():6.1f}  touches/call {(t1 - t0) / n:.1f}", flush=True)
+    for w, xs in pooled.items():
+        x = np.concatenate(xs)
+        print(f"pooled prewarm {w:>5s}: calls {x.size}  p50 {np.percentile(x, 50):6.1f} us  p90 {np.percentile(x, 90):6.1f}  "
+              f"p99 {np.percentile(x, 99):6.1f}  p99.9 {np.percentile(x, 99.9):6.1f}  mean {x.mean():6.1f}", flush=True)
     e.close()
 
 
@@ -610,7 +736,7 @@ def probe_noise_src(model="arm", K="4096", H="32", n="2000"):
 
 PROBES = {"timeline": probe_timeline, "noise_src": probe_noise_src, "peer_soak": probe_peer_soak, "geom": probe_geom, "batch": probe_batch, "fences": probe_fences, "calls": probe_calls,
           "sequence": probe_sequence, "stamps": probe_stamps, "latency": probe_latency,
-          "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate,
+          "ramp": probe_ramp, "peer_ranks": probe_peer_ranks, "rate": probe_rate, "rate_split": probe_rate_split, "rate_prewarm": probe_rate_prewarm,
           "store_floor": probe_store_floor}
 
 if __name__ == "__main__":
