@@ -322,6 +322,27 @@ Step* step_create(int device, std::string* why) {
         if (!step_destroy(s)) *why += " (and the probe's queue did not drain)";
         return nullptr;
     }
+    // step_touch's argument blocks and scratch output, here on the creating thread (whose device
+    // is the queue's): the prewarm thread that touches never selects a device
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!lookup(s->dev, "k_dispatch_probe", &s->kt, why)) { (void)step_destroy(s); return nullptr; }
+    }
+    unsigned char h[128] = {};
+    if (hipMalloc(&s->d_touch, 3 * 64) != hipSuccess) {
+        s->d_touch = nullptr;
+        *why = "touch buffer";
+        (void)step_destroy(s);
+        return nullptr;
+    }
+    unsigned char* outs[2] = {s->d_touch + 128, s->d_touch + 136};
+    memcpy(h, &outs[0], 8);
+    memcpy(h + 64, &outs[1], 8);
+    if (hipMemcpy(s->d_touch, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
+        *why = "touch upload";
+        (void)step_destroy(s);
+        return nullptr;
+    }
     return s;
 }
 
@@ -654,18 +675,6 @@ int step_touch(Step* s, bool if_free, std::string* err) {
         qlk.lock();
     }
     if (s->qerr.load()) { *err = "native queue error: " + hsa_msg((hsa_status_t)s->qerr.load()); return -1; }
-    if (!s->d_touch) {
-        {
-            std::lock_guard<std::mutex> lk(g_mu);
-            if (!lookup(s->dev, "k_dispatch_probe", &s->kt, err)) return -2;
-        }
-        if (hipMalloc(&s->d_touch, 3 * 64) != hipSuccess) { *err = "touch buffer"; s->d_touch = nullptr; return -1; }
-        unsigned char h[128] = {};
-        unsigned char* outs[2] = {s->d_touch + 128, s->d_touch + 136};
-        memcpy(h, &outs[0], 8);
-        memcpy(h + 64, &outs[1], 8);
-        if (hipMemcpy(s->d_touch, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) { *err = "touch upload"; return -1; }
-    }
     mppi::LaunchDesc l{};
     l.grid[0] = l.grid[1] = l.grid[2] = 1;
     l.block[0] = 64; l.block[1] = l.block[2] = 1;

@@ -56,7 +56,7 @@ const char* step_call_memory(Step* s);
 // Two one-wave packets (k_dispatch_probe into a scratch word) on the engine's queue: its
 // packet processor and queue state exercised, no engine buffer touched (the next batch re-uploads
 // its step word: the pair moved the packet indices).  From any thread.  if_free: 1 without
-// touching when another thread holds the queue.  0 / 1 / -2 / -1.
+// touching when another thread holds the queue.  0 / 1 / -1 (a queue error).
 int step_touch(Step* s, bool if_free, std::string* err);
 // The doorbell rung again with the last packet's index: no packet, nothing dispatched.
 // Only from the thread that writes the packets (a stale index rung after a newer one would hide
