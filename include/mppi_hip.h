@@ -353,8 +353,9 @@ mppi_status mppi_synchronize(mppi_engine* e);
  * median interval of the last calls' start times and, from window_us before that until the call
  * starts (at most window_us after it), puts a pair of one-wave packets on the engine's native
  * queue every 25 us; those write a scratch word only, so results are unchanged.  Calls back to back
- * (interval < 4 windows) or slower than 1 s get no touches; with HIP dispatch (no native queue)
- * it does nothing.  The thread spins through each window (2 x window_us of one core per tick).
+ * (interval < 4 windows) or slower than 1 s get no touches; nor do calls that go out as HIP
+ * launches (HIP dispatch, several vehicles, a shard).  Through each window the thread sleeps
+ * between touches (MPPI_PREWARM_SPIN=1, a diagnostic: it spins).
  * window_us: 0 = off (the default), else 50 .. 5000.  mppi_destroy stops it.
  * mppi_get_prewarm: the window and the touches so far. */
 mppi_status mppi_set_prewarm(mppi_engine* e, int32_t window_us);

@@ -566,6 +566,8 @@ static bool probe_dispatch_ids(Step* s, std::string* why) {
     return true;
 }
 
+std::unique_lock<std::recursive_mutex> step_guard(Step* s) { return std::unique_lock<std::recursive_mutex>(s->mu); }
+
 int step_dispatch(Step* s, int n, std::string* err) {
     std::lock_guard<std::recursive_mutex> qlk(s->mu);
     if (!s->valid) { *err = "step_dispatch before step_prepare"; return -1; }

@@ -11,6 +11,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 
 #include "mppi_dev.h"
@@ -39,6 +40,10 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
 // n (rollout, finalize) pairs, each kernel dependent on the one before; the last finalize
 // carries the completion signal and a system-scope release.
 int step_dispatch(Step* s, int n, std::string* err);
+// The queue held against other threads' packets (the prewarm thread's step_touch) while the
+// guard lives: a step_prepare and the step_dispatch after it must see the same packet index,
+// or the batch's rollouts would run later steps than prepared.
+std::unique_lock<std::recursive_mutex> step_guard(Step* s);
 // One control call: a (rollout, finalize) pair whose rollout arguments (the state changes every
 // call) are written by the host into a fresh block of a small ring in host-writable device
 // memory (pinned host memory without one), the finalize's from a static device block.  The host

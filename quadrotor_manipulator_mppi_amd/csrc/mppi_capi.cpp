@@ -427,6 +427,7 @@ struct mppi_engine {
     std::atomic<int64_t> call_t[8];     // steady-clock start of the last 8 control calls (ring)
     std::atomic<int64_t> call_n{0};     // control calls recorded
     bool pw_spin = false;               // diagnostics (MPPI_PREWARM_SPIN=1): spin between touches
+    std::atomic<bool> pw_native{false}; // the last control call went out as native packets
 };
 
 namespace {
@@ -1173,7 +1174,8 @@ void prewarm_loop(mppi_engine* e) {
     while (!e->pw_stop.load()) {
         const int64_t win = (int64_t)e->pw_us.load() * 1000;
         const int64_t n = e->call_n.load(std::memory_order_acquire);
-        if (n < 4 || !e->aql) { nap(2000000); continue; }   // (e->aql is set before the first recorded call ends)
+        // (e->aql is set before the first recorded call ends; calls through HIP launches use no native queue)
+        if (n < 4 || !e->aql || !e->pw_native.load(std::memory_order_relaxed)) { nap(2000000); continue; }
         const int m = (int)std::min<int64_t>(n, 8);
         int64_t t[8], d[8];
         for (int i = 0; i < m; ++i) t[i] = e->call_t[(n - m + i) % 8].load(std::memory_order_relaxed);
@@ -1896,6 +1898,7 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         const auto c0 = std::chrono::steady_clock::now();
         if ((st = control_call_aql(e, state, &used)) != MPPI_OK) return st;
         e->calls_native = used;
+        e->pw_native.store(used, std::memory_order_relaxed);
         if (used) {
             if (!prof) return mppi_read_outputs(e, out, u0, stats);
             const auto c1 = std::chrono::steady_clock::now();
@@ -1913,6 +1916,7 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         }
     }
     e->calls_native = false;
+    e->pw_native.store(false, std::memory_order_relaxed);   // (HIP launches: nothing to prewarm)
     if (state && (st = mppi_set_state(e, state)) != MPPI_OK) return st;
     const float* dn = nullptr;
     if (e->cfg.noise_mode == MPPI_NOISE_INJECTED) {
@@ -2010,6 +2014,7 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     }
     std::string err;
     const auto c2 = now();
+    const auto guard = mppi_aql::step_guard(e->aql);   // (no prewarm touch between prepare and dispatch)
     const int pr = mppi_aql::step_prepare(e->aql, roll, fin, e->step_ctr, kRollStepOff, &err);
     const auto c3 = now();
     if (pr == -2) {   // not dispatchable natively (a kernel the code objects lack, hidden arguments)

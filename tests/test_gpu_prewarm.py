@@ -53,6 +53,20 @@ def test_prewarm_changes_no_result_and_stops():
         o2, u2, _ = warm.step(STATE)
         assert np.array_equal(o1, o2) and np.array_equal(u1, u2)
         time.sleep(period)
+    # batches issued inside the touch window (100 us before the predicted call): touches land
+    # between and around them; each batch's rollouts must still run the steps prepared for them
+    nxt = time.perf_counter()
+    for i in range(30):
+        o1, u1, _ = plain.step(STATE)
+        o2, u2, _ = warm.step(STATE)
+        assert np.array_equal(o1, o2) and np.array_equal(u1, u2), f"window call {i}"
+        nxt += period
+        time.sleep(max(0.0, nxt - 0.0001 - time.perf_counter()))
+        warm.run_steps(2)
+        plain.run_steps(2)
+    warm.synchronize()
+    plain.synchronize()
+    assert np.array_equal(warm.get_u_prev(), plain.get_u_prev())
     warm.set_prewarm(0)
     _, t_off = warm.prewarm()
     for _ in range(10):
