@@ -354,7 +354,8 @@ mppi_status mppi_synchronize(mppi_engine* e);
  * starts (at most window_us after it), puts a pair of one-wave packets on the engine's native
  * queue every 25 us; those write a scratch word only, so results are unchanged.  Calls back to back
  * (interval < 4 windows) or slower than 1 s get no touches; nor do calls that go out as HIP
- * launches (HIP dispatch, several vehicles, a shard).  Through each window the thread sleeps
+ * launches (HIP dispatch, several vehicles, an RCCL or torch-collective shard; a peer-exchange
+ * shard's calls are native).  Through each window the thread sleeps
  * between touches (MPPI_PREWARM_SPIN=1, a diagnostic: it spins).
  * window_us: 0 = off (the default), else 50 .. 5000.  mppi_destroy stops it.
  * mppi_get_prewarm: the window and the touches so far. */
