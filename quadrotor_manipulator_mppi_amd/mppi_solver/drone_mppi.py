@@ -25,8 +25,9 @@ from ._outputs import LazyU, OutputRing
 
 class MPPI(LazyU):
     def __init__(self, n_samples: int = 1000, n_timestep: int = 32, device: Optional[int] = None,
-                 noise: str = "philox", seed: int = 0x5EED, verbose: bool = False):
+                 noise: str = "philox", seed: int = 0x5EED, verbose: bool = False, prewarm_us: int = 0):
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
+        self._prewarm_us = int(prewarm_us)
         self._dev_index = device or 0
         self.n_samples = n_samples
         self.n_timestep = n_timestep
@@ -61,6 +62,8 @@ class MPPI(LazyU):
                           device=self._dev_index)
         self._engine = Engine(cfg)
         self._engine.set_u_prev(u)
+        if self._prewarm_us:   # (mppi_set_prewarm: for a loop ticking with idle gaps)
+            self._engine.set_prewarm(self._prewarm_us)
         return self._engine
 
     @property

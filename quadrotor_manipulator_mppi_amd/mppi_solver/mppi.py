@@ -56,11 +56,13 @@ class MPPI(LazyU):
     def __init__(self, n_samples: int = 100, n_horizon: int = 32, device: Optional[int] = None,
                  noise: str = "philox", seed: int = 0x5EED, urdf_path: Optional[str] = None,
                  root_link: str = "base", end_link: str = "j2s7s300_link_7", verbose: bool = True,
-                 cost_terms=(), cost_weights=None):
+                 cost_terms=(), cost_weights=None, prewarm_us: int = 0):
         """``cost_terms``: CostManager terms to switch on beyond the pose cost the
         reference runs (cost_manager.py:83-87): any of ``covar, center, joint_track,
         action, joint_limit`` (engine.COST_TERMS); ``cost_weights`` overrides their
-        weights (defaults: cost_manager.py:21-43)."""
+        weights (defaults: cost_manager.py:21-43).  ``prewarm_us`` > 0: the engine's queue
+        prewarm with that window (mppi_set_prewarm), for a node ticking with idle gaps such as
+        kinova.py:101's rospy.Rate(100); results are unchanged."""
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
         self._dev_index = device or 0
         # mppi.py:37-42
@@ -73,6 +75,7 @@ class MPPI(LazyU):
         self._lambda = 0.1
         self._noise, self._seed = noise, seed
         self._cost_terms, self._cost_weights = cost_terms, cost_weights
+        self._prewarm_us = int(prewarm_us)
         self.verbose = verbose
         self.chain = parse_urdf_chain(urdf_path, root_link, end_link) if urdf_path else load_chain()
         # mppi.py:45-58
@@ -110,6 +113,8 @@ class MPPI(LazyU):
                           cost_terms=self._cost_terms, cost_weights=self._cost_weights)
         self._engine = Engine(cfg)
         self._engine.set_u_prev(u)
+        if self._prewarm_us:
+            self._engine.set_prewarm(self._prewarm_us)
         return self._engine
 
     @property

@@ -26,9 +26,10 @@ from ._outputs import LazyU, OutputRing
 class MPPI(LazyU):
     def __init__(self, n_samples: int = 1000, n_timestep: int = 32, device: Optional[int] = None,
                  noise: str = "philox", seed: int = 0x5EED, mass: float = 14.7,
-                 inertia=(1.57, 3.93, 2.59), kd: float = 0.0, gravity: float = 9.81, verbose: bool = False):
+                 inertia=(1.57, 3.93, 2.59), kd: float = 0.0, gravity: float = 9.81, verbose: bool = False, prewarm_us: int = 0):
         self.device = torch.device(f"cuda:{device or 0}" if torch.cuda.is_available() else "cpu")
         self._out_ring = OutputRing(self.device, 12)   # (x_des, v_des): one async H2D copy per call
+        self._prewarm_us = int(prewarm_us)
         self._dev_index = device or 0
         self.n_samples = n_samples
         self.n_timestep = n_timestep
@@ -63,6 +64,8 @@ class MPPI(LazyU):
                           device=self._dev_index, quad=self.params)
         self._engine = Engine(cfg)
         self._engine.set_u_prev(u)
+        if self._prewarm_us:   # (mppi_set_prewarm: for a loop ticking with idle gaps)
+            self._engine.set_prewarm(self._prewarm_us)
         return self._engine
 
     @property

@@ -82,3 +82,24 @@ def test_prewarm_changes_no_result_and_stops():
         time.sleep(0.002)
     warm.close()
     plain.close()
+
+
+def test_dropin_prewarm_option_changes_nothing():
+    """The drop-in arm class with ``prewarm_us`` (the node's 100 Hz loop, kinova.py:101-116) returns
+    what the class without it returns, and its engine touches its queue between the ticks."""
+    import torch
+    from quadrotor_manipulator_mppi_amd.mppi_solver.mppi import MPPI
+    q = torch.tensor([0, 0, 1, 0, 0, 0, 1] + HOME, dtype=torch.float64)
+    v = torch.zeros(13, dtype=torch.float64)
+    plain, warm = MPPI(n_samples=256, verbose=False), MPPI(n_samples=256, verbose=False, prewarm_us=200)
+    nxt = time.perf_counter()
+    for i in range(30):
+        for m in (plain, warm):
+            m.update_joint(q, v)
+        q1, v1 = plain.compute_control_input()
+        q2, v2 = warm.compute_control_input()
+        assert torch.equal(torch.as_tensor(q1), torch.as_tensor(q2)) and torch.equal(torch.as_tensor(v1), torch.as_tensor(v2)), i
+        nxt += 0.003
+        time.sleep(max(0.0, nxt - time.perf_counter()))
+    assert warm._engine.prewarm()[0] == 200 and warm._engine.prewarm()[1] > 0
+    assert plain._engine.prewarm() == (0, 0)
