@@ -1174,8 +1174,9 @@ void prewarm_loop(mppi_engine* e) {
     while (!e->pw_stop.load()) {
         const int64_t win = (int64_t)e->pw_us.load() * 1000;
         const int64_t n = e->call_n.load(std::memory_order_acquire);
-        // (e->aql is set before the first recorded call ends; calls through HIP launches use no native queue)
-        if (n < 4 || !e->aql || !e->pw_native.load(std::memory_order_relaxed)) { nap(2000000); continue; }
+        // pw_native (acquire) first: a native call stored it (release) after e->aql was set, so the
+        // pointer is read only once its write is visible here.  HIP-launched calls: nothing to warm.
+        if (n < 4 || !e->pw_native.load(std::memory_order_acquire) || !e->aql) { nap(2000000); continue; }
         const int m = (int)std::min<int64_t>(n, 8);
         int64_t t[8], d[8];
         for (int i = 0; i < m; ++i) t[i] = e->call_t[(n - m + i) % 8].load(std::memory_order_relaxed);
@@ -1898,7 +1899,7 @@ mppi_status mppi_step(mppi_engine* e, const double* state, const float* h_noise,
         const auto c0 = std::chrono::steady_clock::now();
         if ((st = control_call_aql(e, state, &used)) != MPPI_OK) return st;
         e->calls_native = used;
-        e->pw_native.store(used, std::memory_order_relaxed);
+        e->pw_native.store(used, std::memory_order_release);
         if (used) {
             if (!prof) return mppi_read_outputs(e, out, u0, stats);
             const auto c1 = std::chrono::steady_clock::now();
