@@ -1167,6 +1167,21 @@ void note_call(mppi_engine* e) {   // mppi_step entry (the caller's thread)
     e->call_n.store(n + 1, std::memory_order_release);
 }
 
+// The next window from the last m (<= 8) call starts t[] (oldest first): the median interval P
+// predicts the call at t[m-1] + P, the window is [that - win, that + win].  0: no window (fewer
+// than 4 calls, P < 4 windows -- back to back -- or P > 1 s); 1: *start / *end set.
+int prewarm_plan(const int64_t* t, int m, int64_t win, int64_t* start, int64_t* end) {
+    if (m < 4) return 0;
+    int64_t d[8];
+    for (int i = 1; i < m; ++i) d[i - 1] = t[i] - t[i - 1];
+    std::nth_element(d, d + (m - 1) / 2, d + (m - 1));
+    const int64_t P = d[(m - 1) / 2];
+    if (P < 4 * win || P > 1000000000) return 0;
+    *start = t[m - 1] + P - win;
+    *end = t[m - 1] + P + win;
+    return 1;
+}
+
 void prewarm_loop(mppi_engine* e) {
     prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);   // this thread's sleeps end ~1 us after their deadline
     std::unique_lock<std::mutex> lk(e->pw_mu);
@@ -1178,13 +1193,10 @@ void prewarm_loop(mppi_engine* e) {
         // pointer is read only once its write is visible here.  HIP-launched calls: nothing to warm.
         if (n < 4 || !e->pw_native.load(std::memory_order_acquire) || !e->aql) { nap(2000000); continue; }
         const int m = (int)std::min<int64_t>(n, 8);
-        int64_t t[8], d[8];
+        int64_t t[8], start = 0, end = 0;
         for (int i = 0; i < m; ++i) t[i] = e->call_t[(n - m + i) % 8].load(std::memory_order_relaxed);
-        for (int i = 1; i < m; ++i) d[i - 1] = t[i] - t[i - 1];
-        std::nth_element(d, d + (m - 1) / 2, d + (m - 1));
-        const int64_t P = d[(m - 1) / 2], last = t[m - 1];
-        const int64_t start = last + P - win, end = last + P + win, now = steady_ns();
-        if (P < 4 * win || P > 1000000000 || now > end) { nap(2000000); continue; }   // no cadence, or the call is late
+        const int64_t now = steady_ns();
+        if (!prewarm_plan(t, m, win, &start, &end) || now > end) { nap(2000000); continue; }   // no cadence, or the call is late
         if (now < start - 200000) { nap(start - 100000 - now); continue; }           // (then look again)
         lk.unlock();   // through the window: a touch, then sleep to the next (the host keeps its core)
         int64_t next = start;
@@ -2453,6 +2465,13 @@ int32_t mppi_debug_queue_touch(mppi_engine* e) {
     std::string err;
     const int r = mppi_aql::step_touch(e->aql, false, &err);
     return r == 0 ? MPPI_OK : fail(MPPI_ERR_HIP, "queue touch: %s", err.c_str());
+}
+
+// Diagnostic (host only, tests/test_capi_cpu.py): the prewarm thread's window for call starts
+// t[0..m) in ns and a window of window_us: 1 and [*start, *end], or 0 (no window).
+int32_t mppi_debug_prewarm_plan(const int64_t* t, int32_t m, int32_t window_us, int64_t* start, int64_t* end) {
+    if (!t || !start || !end || m < 0 || m > 8) return MPPI_ERR_INVALID_ARG;
+    return prewarm_plan(t, m, (int64_t)window_us * 1000, start, end);
 }
 
 // Diagnostic: mppi_aql step_ring (the doorbell again, no packet).
