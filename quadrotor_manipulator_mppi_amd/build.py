@@ -42,8 +42,9 @@ SOURCES = [(u, f + (_MAXILP if u in _XI else [])) for u, f in
            [("mppi_rollout_drone.hip", _ROLL), ("mppi_rollout_arm.hip", _ROLL), ("mppi_rollout_arm32.hip", _ROLL),
             ("mppi_rollout_wb.hip", _ROLL), ("mppi_finalize.hip", _FIN)]] + \
           [("mppi_rollout_arm_h32.hip", _ROLL + _MAXILP + os.environ.get("MPPI_C3_EXTRA", "").split()), ("mppi_rollout_quad.hip", _ROLL + _MAXILP),
-           ("mppi_capi.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
-HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h",
+           ("mppi_host_math.cpp", []), ("mppi_engine.cpp", []), ("mppi_step.cpp", []), ("mppi_exchange.cpp", []),
+           ("mppi_prewarm.cpp", []), ("mppi_dynamics.cpp", []), ("mppi_aql.cpp", [])]
+HEADERS = ["mppi_dev.h", "mppi_device.h", "mppi_rollout.h", "mppi_aql.h", "mppi_engine.h",
            os.path.join("..", "..", "include", "mppi_hip.h")]
 # Native dispatch (mppi_aql.cpp) loads each kernel unit's gfx950 code object from next to the
 # library: <library stem>.<unit>.co, built from the same source with the same flags.

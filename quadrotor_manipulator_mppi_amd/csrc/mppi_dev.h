@@ -1,4 +1,4 @@
-// mppi_dev.h -- structures shared by the host C-ABI (mppi_capi.cpp) and the
+// mppi_dev.h -- structures shared by the host C-ABI (mppi_engine.h and its .cpp units) and the
 // gfx950 kernels (mppi_kernels.hip).  Internal: not part of the public ABI.
 #pragma once
 #include <stddef.h>
@@ -158,7 +158,7 @@ struct FinTail {
 // stand, nothing else written)
 enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTailSlots = 4 };
 
-// Peer exchange of a sharded V == 1 engine (mppi_capi.cpp mppi_peer_open / mppi_peer_connect):
+// Peer exchange of a sharded V == 1 engine (mppi_exchange.cpp mppi_peer_open / mppi_peer_connect):
 // every k_finalize block pushes its partial -- header (rho, eta, eta2, nan) and its window's
 // columns N[t] -- into every rank's exchange region, and gathers the ranks' partials of the same
 // block from its own.  Each word is 8 B, (value bits, tag): one store carries its own validity,

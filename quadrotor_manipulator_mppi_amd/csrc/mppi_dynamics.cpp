@@ -27,7 +27,7 @@
 
 #include "../../include/mppi_hip.h"
 
-extern "C" mppi_status mppi_fail_dyn(mppi_status st, const char* msg);   // mppi_capi.cpp (last_error)
+extern "C" mppi_status mppi_fail_dyn(mppi_status st, const char* msg);   // mppi_host_math.cpp (last_error)
 
 namespace {
 

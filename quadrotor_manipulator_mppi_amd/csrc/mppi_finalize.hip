@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         double o1 = 0.0, o2 = 0.0;   // this dim's two outputs (position, velocity)
         if (model == MPPI_MODEL_QUADROTOR) {
             // coupled dims (thrust rotated by R(rpy)): the host forms the outputs from u0
-            // (mppi_capi.cpp quad_outputs)
+            // (mppi_engine.cpp quad_outputs)
         } else if (drone_dim) {   // drone_mppi.py:168-169
             const float x0 = x0f, v0 = v0f;
             const float xo = (x0 + v0 * dt) + (0.5f * u0) * dt2;
@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // output records in mapped host memory, each ONE 16 B store carrying the step's sequence
         // number beside its values -- (o1, u0, seq) and (o2, nan flag, seq) per dim, (rho, eta,
         // ess, seq) per vehicle -- so the host takes the values from a record whose own tag it
-        // checks (mppi_capi.cpp wait_outputs / mppi_read_outputs) and nothing needs ordering
+        // checks (mppi_step.cpp wait_outputs / mppi_read_outputs) and nothing needs ordering
         // against anything else: no system-scope fence (an L2 writeback of ~1.5 us of kernel
         // time on the call's latency path) and no separate flag store.  The plain arrays above
         // stay for the native batches (completed by their packet's system-scope release).

@@ -24,7 +24,7 @@ from quadrotor_manipulator_mppi_amd.distributed import (HDR, all_reduce_slots, c
 
 
 def _slot_len(A, H):
-    return (HDR + A * H + 3) & ~3   # P: header + N[a][t], rounded to 16 B (mppi_capi.cpp)
+    return (HDR + A * H + 3) & ~3   # P: header + N[a][t], rounded to 16 B (mppi_engine.cpp)
 
 
 def _pack(S, eps, lam, P):

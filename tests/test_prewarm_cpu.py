@@ -1,4 +1,4 @@
-"""The prewarm thread's cadence prediction (mppi_capi.cpp prewarm_plan, through the diagnostic
+"""The prewarm thread's cadence prediction (mppi_prewarm.cpp prewarm_plan, through the diagnostic
 mppi_debug_prewarm_plan; host code only, no GPU): from the last call starts it predicts the next
 call of a node that ticks at a fixed rate (kinova.py:101, rospy.Rate(100)) and opens a window of
 +- window_us around it; no window for fewer than 4 calls, back-to-back calls or a cadence slower
