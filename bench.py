@@ -5,6 +5,7 @@ state-steps, plus control-step p50 latency).
     python bench.py [--gpus 1] [--steps K] [--warmup W] [--workload arm_c3]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N ...
+    python bench.py --gpus N ...      (no launcher: bench.py starts the N ranks itself, as a child)
 
 A "step" is one MPPI control step (noise -> rollout -> FK -> cost -> softmin ->
 SavGol -> update) over one batch of synthetic state/goal input.
@@ -80,6 +81,11 @@ WORKLOADS = {
     "c4_shard_peer1": dict(model="wholebody", n_samples=8192, n_horizon=64, native=True, mode="peer",
                            desc="Whole-body 8192 samples H=64 through the 1-rank peer exchange "
                                 "(the N=8 rank's step of BASELINE configs[3])"),
+    # configs[3] through the mechanism north_star names, "a single RCCL allreduce": the C4 split
+    # 65536/N per rank, the engine-owned RCCL communicator over all N ranks (one ncclAllReduce per step)
+    "c4_rccl": dict(model="wholebody", n_samples=C4_K_TOTAL, n_horizon=64, strong=True, native=True, mode="rccl",
+                    desc="Whole-body MPPI K=65536 H=64, samples split K/N per GPU, one RCCL all-reduce per step "
+                         "(BASELINE configs[3], the north star's mechanism)"),
 }
 
 # the CPU baseline's shapes (C4 K-reduced: the full C4 on CPU is impractical)
@@ -96,6 +102,72 @@ CPU_HEADLINE = {"arm_c3": "c3_arm_k4096_h32", "drone_c2": "c2_drone_k4096_h32",
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------------------ N ranks from one command
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n: int, argv, port: int = 0, script: str = ""):
+    """The child that runs ``bench.py <argv>`` as N ranks on this node: torch.distributed.run with a
+    static rendezvous on 127.0.0.1 (the driver's own launch line), every argument forwarded as given."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()),
+            script or os.path.abspath(__file__)] + list(argv)
+
+
+def is_bench_line(s: str) -> bool:
+    try:
+        d = json.loads(s)
+    except ValueError:
+        return False
+    return isinstance(d, dict) and "metric" in d and "value" in d
+
+
+def spawn_ranks(cmd, out=None) -> int:
+    """``bench.py --gpus N`` (N > 1) started without a launcher: run ``cmd`` (``launcher_cmd``) as a
+    CHILD process -- never exec, this process has not touched the GPU and stays the parent -- relay
+    exactly one bench line from the child's stdout (rank 0's; anything else there goes to stderr)
+    and return the child's exit code.  SIGTERM / SIGINT to this process are passed on to the child's
+    process group, so a driver that stops the parent stops the ranks too."""
+    import signal
+    import subprocess
+    out = out or sys.stdout
+    env = dict(os.environ, MPPI_BENCH_SPAWNED="1")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    log(f"bench: no launcher in the environment, starting the ranks as a child: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+
+    def forward(sig, _frame):
+        try:
+            os.killpg(proc.pid, sig)
+        except OSError:
+            pass
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = []
+    try:
+        for ln in proc.stdout:
+            s = ln.strip()
+            if is_bench_line(s):
+                lines.append(s)
+            elif s:
+                log(f"[child stdout] {s}")
+        rc = proc.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    if len(lines) > 1:
+        log(f"bench: the child printed {len(lines)} bench lines; relaying the last")
+    if lines:
+        print(lines[-1], file=out, flush=True)
+    elif rc == 0:
+        log("bench: the ranks exited 0 without a bench line")
+        rc = 1
+    return rc
 
 
 def build_info():
@@ -433,6 +505,11 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
     if not os.environ.get("MPPI_FIN_DEBUG"):
         assert np.isfinite(out).all(), "non-finite control output"
     comm = eng.comm_info() if se.mode == "rccl" else None
+    # the peer exchange's own rank count: the ranks whose word reached this rank's region in the
+    # connection probe's kernel phase (mppi_peer_info), min over ranks
+    peer_n = None
+    if se.mode == "peer":
+        peer_n = int(-reduce_max([-float(eng.peer_info()[0])], dist, red_dev)[0])
     res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
            "lat100_prewarm": lat100p, "prewarm_touches": pw_touches,
            "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
@@ -441,7 +518,10 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
            "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native, "exchange": se.mode,
            "native_error": se.native_error, "world": world,
            "backend": dist.get_backend() if dist is not None else None,
-           "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None}
+           "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None,
+           "peer_ranks_connected": peer_n, "agree_every": se.agree_every if se.mode == "peer" and world > 1 else None,
+           "process_group": ({"backend": dist.get_backend(), "size": dist.get_world_size()} if dist is not None
+                             else None)}
     eng.close()
     return res
 
@@ -568,6 +648,13 @@ def make_line(workload, r, args, secondary=None, cpu=None, cpu_all=None, measure
                            "vehicles": "none: the fleet's vehicles split over the ranks (each rank a whole "
                                        "controller of its vehicles), nothing exchanged"}[r["exchange"]],
             "allreduce_us": tim.get("allreduce_us") if tim else None,
+            "peer_ranks_connected": r.get("peer_ranks_connected"),
+            "peer_ranks_connected_source": ("mppi_peer_info: ranks whose tagged word reached this rank's region in the "
+                                            "connection probe's kernel phase, min over ranks")
+                                           if r.get("peer_ranks_connected") is not None else None,
+            "peer_agree_every": r.get("agree_every"),
+            "process_group": r.get("process_group"),
+            "ranks_per_gpu": r.get("ranks_per_gpu"),
             "native_comm_error": r["native_error"],
             "rollout_us_max_over_ranks": tim.get("rollout_in_step_us_max_over_ranks") if tim else None,
             "payload_bytes_per_rank": int((4 + r["A"] * H + 3) // 4 * 4 * 4 * V)}
@@ -609,9 +696,11 @@ def secondary_entry(s, ns):
          "roofline_frac_step": rf["frac_step"]}
     if s["native"]:
         e.update({"exchange": s.get("exchange", "rccl"), "allreduce_us": s["tim"].get("allreduce_us"),
-                  "rccl_nranks": s["rccl_nranks"]})
+                  "rccl_nranks": s["rccl_nranks"], "peer_ranks_connected": s.get("peer_ranks_connected")})
     if s["world"] > 1:
         e.update({"exchange": s["exchange"], "native_comm_error": s["native_error"],
+                  "rccl_nranks": s["rccl_nranks"], "peer_ranks_connected": s.get("peer_ranks_connected"),
+                  "process_group": s.get("process_group"),
                   "rollout_us_max_over_ranks": s["tim"].get("rollout_in_step_us_max_over_ranks")})
     if s.get("exchange") == "vehicles":   # the fleet split over the ranks: no exchange at all
         e.update({"exchange": "none", "split": "vehicles", "vehicles_total": s["world"] * s["V"], "samples_total": s["K"],
@@ -666,9 +755,15 @@ def main():
     ap.add_argument("--secondary", default="drone_c2,wholebody_c4,c4_shard_native1,c4_shard_peer1,c4,fleet_c5,"
                                            "fleet_c5_share,quadrotor_c2",
                     help="extra workloads reported at N=1, comma separated; '' for none")
-    ap.add_argument("--secondary-multi", default="c4,fleet_c5",
+    ap.add_argument("--secondary-multi", default="c4,c4_rccl,fleet_c5",
                     help="extra workloads reported at N>1 (every rank runs them), comma separated; '' for none")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # N ranks from one command: the ranks run as a child (torch.distributed.run), this process
+        # relays rank 0's line and exits with the child's code (nothing here has touched the GPU)
+        if os.environ.get("MPPI_BENCH_SPAWNED"):
+            raise SystemExit("bench.py: started by its own launcher without WORLD_SIZE")
+        sys.exit(spawn_ranks(launcher_cmd(args.gpus, sys.argv[1:])))
     # the JSON line is the only thing on stdout: keep the real stdout for it and send fd 1 to
     # stderr, so native libraries that print there (RCCL's version banner at communicator
     # init) cannot add lines to it
@@ -693,11 +788,17 @@ def main():
         binding = bind_to_gpu_numa(local)
         log(f"cpu binding: {binding}")
     dist = None
+    ndev = torch.cuda.device_count()   # (no GPU initialisation on this image)
+    ranks_per_gpu = -(-world // max(1, ndev))
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        backend = os.environ.get("MPPI_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only for rehearsal
+        # nccl = RCCL; with more ranks than GPUs (a rehearsal of N ranks on fewer GPUs, which RCCL
+        # cannot pair) the process group is gloo
+        backend = os.environ.get("MPPI_DIST_BACKEND", "nccl" if world <= ndev else "gloo")
+        if world > ndev:
+            log(f"note: {world} ranks on {ndev} GPU(s): a rehearsal, process group {backend}")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -712,12 +813,14 @@ def main():
     batches = args.batches or auto_batches(args.steps)
     r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
                      timing=not args.no_kernel_timing, batches=batches, lat_rate_calls=args.latency_steps)
+    r["ranks_per_gpu"] = ranks_per_gpu
     secondary = {}
     extra = args.secondary if world == 1 else args.secondary_multi
     if extra and r["tim"] is not None:
         for wname in [s for s in extra.split(",") if s and s != workload]:
             ns = max(50, args.steps // 5)
             s = run_workload(wname, ns, 20, world, dist, 50, batches=3)   # (every rank, in lockstep)
+            s["ranks_per_gpu"] = ranks_per_gpu
             secondary[wname] = secondary_entry(s, ns)
             log(f"secondary {wname}: {secondary[wname]}")
     dropin = None

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 8
+#define MPPI_ABI_VERSION 9
 #define MPPI_COMM_ID_BYTES 128  /* ncclUniqueId */
 #define MPPI_PEER_HANDLE_BYTES 64  /* hipIpcMemHandle_t */
 #define MPPI_MAX_ACTION 16
@@ -267,18 +267,20 @@ mppi_status mppi_exchange(mppi_engine* e);
  * step's): a control step is the unsharded step's two kernels (native dispatch included), no
  * PACK launch, no host-enqueued collective.  Every rank finalises bit-identically, and one
  * rank reproduces the unsharded engine exactly.
- * Failure handling.  A block that waits 2 s for a peer gives the step up: the step keeps the warm
- * start (w_eps = 0), and the block reports the timeout three ways -- into the control word of this
- * rank in EVERY rank's region, as the step's abort tag over its header words in the peers' regions
- * (a peer still polling that step gives it up too), and into this engine's sticky word.  From then
- * on every rank's finalize blocks find the report in their own region and give every step up at
- * once (u_prev held on every rank, no 2 s waits) until the host resets the exchange, so no rank
+ * Failure handling.  A block that waits 2 s for a peer proposes to give the step up; within a rank
+ * the step is all or nothing (mppi_peer_info): the first block's proposal decides for every block
+ * of the rank, so either every slice of u_prev is updated or every one is kept (w_eps = 0).  A rank
+ * that gives the step up reports it twice -- into the control word of this rank in EVERY rank's
+ * region (a peer still polling that step gives it up too) and into this engine's sticky word.  From
+ * then on every rank's finalize blocks find the report in their own region and give every step up
+ * at once (u_prev held on every rank, no 2 s waits) until the host resets the exchange, so no rank
  * keeps updating a warm start the others did not.  The host sees it as stats nonfinite = 2 from
  * mppi_read_outputs (this step's flag on any dim, or the sticky word: any block of any step of a
  * batch), as MPPI_ERR_PEER_TIMEOUT from mppi_synchronize, and through mppi_peer_status (this rank's
  * sticky word and every rank's report as stored in this rank's region).  Recovery is collective
- * (distributed.py ShardedEngine.resync): agree over the process group, take rank 0's warm start,
- * step counter and epoch, and call mppi_peer_reset on every rank between two barriers.
+ * (distributed.py ShardedEngine.resync): agree over the process group, take the warm start, step
+ * counter and epoch of the lowest rank that is not torn (rank 0 normally), and call mppi_peer_reset
+ * on every rank between two barriers.
  * Every rank must run the same sequence of steps with the same step counter (the tags are the
  * Philox counter): a rank that skips a step or rewinds its counter alone leaves the others
  * waiting out the 2 s bound.  mppi_get_weighted_noise gathers the last exchanged step's
@@ -306,6 +308,15 @@ mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase);
  * reports in this rank's region, word r from rank r (tag << 32 | 1, 0 = none; a device-to-host copy
  * after the engine's work); epoch (may be NULL) = the exchange epoch of the tags. */
 mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports, uint32_t* epoch);
+/* The connection and the warm start's integrity (ABI 9): connected = the ranks whose tagged word
+ * reached this rank's region in mppi_peer_probe's kernel phase (phase 2; 0 before it), rank = this
+ * engine's shard_rank, torn (may be NULL) = the step tag of a step this rank's warm start came out
+ * of torn, 0 = none.  Within a rank a step is all or nothing: its finalize blocks decide once,
+ * through a compare-and-swap in the rank's own region, whether every block updates its slice of
+ * u_prev or every block keeps it; a block that timed out on a rank whose other blocks already
+ * updated keeps polling for a second 2 s bound, and only if that passes too is the warm start torn
+ * (the resync then takes its u_prev from a rank that is not torn). */
+mppi_status mppi_peer_info(mppi_engine* e, int32_t* connected, int32_t* rank, uint32_t* torn);
 /* Collective recovery after a timeout: with every rank's engine synchronised and a barrier passed
  * (no kernel writes into any region), clear this rank's region and sticky word and take the step
  * counter and epoch the ranks agreed on; a second barrier follows before any rank steps again. */

@@ -21,7 +21,7 @@ NOISE_PHILOX, NOISE_INJECTED = 0, 1
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FLOATING = 0, 1, 2, 3
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_NONFINITE, ERR_STATE, ERR_COMM, ERR_PEER_TIMEOUT = 0, -1, -2, -3, -4, -5, -6
 COST_COVAR, COST_CENTER, COST_JOINT_TRACK, COST_ACTION, COST_JOINT_LIMIT = 1, 2, 4, 8, 16
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_PEERS = 8
 COMM_ID_BYTES = 128
 PEER_HANDLE_BYTES = 64
@@ -110,6 +110,7 @@ PROTOTYPES = {
     "mppi_peer_connect_ptrs": (_ST, [_P, C.POINTER(C.c_uint64)]),
     "mppi_peer_status": (_ST, [_P, _U32, C.POINTER(C.c_uint64), _U32]),
     "mppi_peer_reset": (_ST, [_P, C.c_uint32, C.c_uint32]),
+    "mppi_peer_info": (_ST, [_P, _I32, _I32, _U32]),
     "mppi_comm_info": (_ST, [_P, _I32, _I32]),
     "mppi_exchange": (_ST, [_P]),
     "mppi_read_outputs": (_ST, [_P, _D, _F, C.POINTER(Stats)]),

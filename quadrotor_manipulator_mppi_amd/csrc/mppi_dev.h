@@ -150,7 +150,9 @@ struct FinTail {
     unsigned long long* const* xpeers;   // peer exchange (mppi_peer_connect): every rank's region, null = off
     unsigned long long* xlocal;          //   this rank's region (the ranks' partials are gathered from it)
     int32_t xn, xme;                     //   rank count, this rank
-    uint32_t* xerr;                      //   sticky timeout word (mapped host memory; read on the late path only)
+    uint32_t* xerr;                      //   sticky timeout word, then the torn word (mapped host memory;
+                                         //   read on the late path only)
+    uint32_t* xstall;                    //   diagnostics (mppi_debug_peer_stall): a block's stall, null = none
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
@@ -173,15 +175,30 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // bits).  The rollout's block 0 hands the counter to the finalize in the vehicle constants (word
 // kVcStepWord); the host puts the epoch there (kVcEpochWord; mppi_set_step_counter and
 // mppi_peer_reset move it), so words a rank left in a region before its counter was rewound can
-// never pass for a later step's.  Bit 30 marks an abort: a block that gives up a step overwrites
-// its header words in the peers' regions with the step's abort tag, and a peer still polling that
-// step gives it up too.
+// never pass for a later step's.  A block that gives a step up leaves the peers' words where they
+// are (a peer block on a rank that committed may still need them, below): the report alone tells
+// a peer still polling that step to give it up too.
+// All or nothing within a rank: the blocks of one step decide ONCE, per rank, whether the step
+// commits (every block updates its slice of u_prev) or is given up (every block keeps it).  Control
+// word kXDec + (step & 1) of the rank's own region holds the decision, (tag << 32) | kDecCommit or
+// kDecGiveUp, set by the first block's compare-and-swap (a block whose peers' words all arrived
+// proposes commit; a block that timed out or saw a report proposes give-up) and adopted by every
+// other block: a block that got its words on a rank that gave up holds its slice, and a block that
+// timed out on a rank that committed keeps polling its peers for a second bound (reports not heeded:
+// the peers' words stay in place) and completes.  Only if that second bound passes too is the rank's
+// warm start torn (that slice held, the others updated); the block then writes the step's tag into
+// the torn word next to the sticky word, and the resync takes its warm start from a rank that is
+// not torn.  Each step's first block clears the other parity's word (the previous step's: every
+// block of it has ended, the kernels of a queue run in order).
 constexpr int kMaxPeers = 8;
 constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
-constexpr int kXCtl = 16;        // control words at the head of a region (8 B each; kMaxPeers used)
+constexpr int kXCtl = 16;        // control words at the head of a region (8 B each): kMaxPeers timeout
+                                 // reports, then the two step parities' decision words
+constexpr int kXDec = kMaxPeers;
+constexpr uint32_t kDecCommit = 1u, kDecGiveUp = 2u;
 constexpr int kVcStepWord = (int)(offsetof(VehicleConst, _pad) / 4) + 1;
 constexpr int kVcEpochWord = kVcStepWord + 1;
-constexpr uint32_t kTagValid = 0x80000000u, kTagAbort = 0x40000000u;
+constexpr uint32_t kTagValid = 0x80000000u;
 // (constexpr: usable from host and device code alike)
 constexpr inline uint32_t peer_tag(uint32_t step, uint32_t epoch) {
     return kTagValid | ((epoch & 0x3FFu) << 20) | (step & 0xFFFFFu);
@@ -230,7 +247,8 @@ struct FinParams {
     unsigned long long* const* xpeers;   // peer exchange (FinTail): the ranks' regions, this rank's,
     unsigned long long* xlocal;          //   rank count, this rank; xpeers null = off
     int32_t xn, xme;
-    uint32_t* xerr;                      //   sticky timeout word (mapped host memory)
+    uint32_t* xerr;                      //   sticky timeout word, torn word (mapped host memory)
+    uint32_t* xstall;                    //   diagnostics: a block's stall (mppi_debug_peer_stall), null = none
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

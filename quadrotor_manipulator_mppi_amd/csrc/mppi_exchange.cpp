@@ -305,10 +305,13 @@ mppi_status mppi_peer_probe(mppi_engine* e, int32_t phase) {
         if (he != hipSuccess) return fail(MPPI_ERR_HIP, "peer probe kernel: %s", hipGetErrorString(he));
         HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
         HIP_TRY(hipDeviceSynchronize());
-        for (int r = 0; r < n; ++r)
+        e->x_connected = 0;
+        for (int r = 0; r < n; ++r) {
             if ((uint32_t)(got[r] >> 32) != (tag | (uint32_t)r))
                 return fail(MPPI_ERR_COMM, "peer exchange: rank %d's word did not reach this rank's region in the "
                                            "kernel probe (%016llx)", r, got[r]);
+            ++e->x_connected;
+        }
         return MPPI_OK;
     }
     auto pattern = [](int r, int d) { return (0x5A5A0000ull | (unsigned)(16 * r + d)) << 32 | 0x3F800000ull; };
@@ -349,6 +352,39 @@ mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports
     return MPPI_OK;
 }
 
+// The connection as the kernel probe saw it and the torn word (mppi_dev.h kXDec): connected = the
+// ranks whose tagged word reached this rank's region in mppi_peer_probe's phase 2 (0 before it).
+mppi_status mppi_peer_info(mppi_engine* e, int32_t* connected, int32_t* rank, uint32_t* torn) {
+    if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
+    if (!e->d_xregion) return fail(MPPI_ERR_STATE, "mppi_peer_info before mppi_peer_open");
+    if (connected) *connected = e->x_connected;
+    if (rank) *rank = e->cfg.shard_rank;
+    if (torn) *torn = e->h_out ? *(const volatile uint32_t*)(e->h_out + off_xerr(e) + 4) : 0u;
+    return MPPI_OK;
+}
+
+// Diagnostic (not part of the public header): the next FINAL's finalize block `block` stalls `ms`
+// milliseconds before it stores its partial into the peers' regions (once; the word is then
+// cleared by the kernel).  The stall word is allocated at the first call, so an engine that never
+// calls this carries a null pointer (no load in the kernel).  tests/test_gpu_peer.py.
+int32_t mppi_debug_peer_stall(mppi_engine* e, int32_t block, int32_t ms) {
+    if (!e || block < 0 || block > 0xFFFF || ms < 0 || ms > 60000) return fail(MPPI_ERR_INVALID_ARG, "bad arguments");
+    if (!e->peer) return fail(MPPI_ERR_STATE, "mppi_debug_peer_stall before mppi_peer_connect");
+    if (use_device(e)) return MPPI_ERR_HIP;
+    if (!e->d_xstall) {
+        HIP_TRY(hipMalloc(&e->d_xstall, sizeof(uint32_t)));
+        e->fp.xstall = e->d_xstall;
+        FinTail t = tail_of(e->fp, 0);
+        t.wraw = t.wsmooth = nullptr;   // (as at create)
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(hipMemcpy(e->d_tail + kTailFinal, &t, sizeof(FinTail), hipMemcpyHostToDevice));
+        e->call_cached = e->batch_cached = false;
+    }
+    const uint32_t w = ms ? ((uint32_t)ms << 16) | (uint32_t)block : 0u;
+    HIP_TRY(hipMemcpy(e->d_xstall, &w, sizeof(w), hipMemcpyHostToDevice));
+    return MPPI_OK;
+}
+
 // Collective recovery after a timeout (distributed.py ShardedEngine.resync): every rank has
 // synchronised its engine and passed a barrier, so no kernel writes into any region; each rank
 // clears its own region (partials and timeout reports) and its sticky word, and takes the step
@@ -360,7 +396,8 @@ mppi_status mppi_peer_reset(mppi_engine* e, uint32_t step, uint32_t epoch) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
     HIP_TRY(hipDeviceSynchronize());
-    *(volatile uint32_t*)(e->h_out + off_xerr(e)) = 0u;
+    *(volatile uint32_t*)(e->h_out + off_xerr(e)) = 0u;       // the sticky word
+    *(volatile uint32_t*)(e->h_out + off_xerr(e) + 4) = 0u;   // the torn word
     e->step_ctr = step;
     e->x_epoch = epoch;
     return build_vehicle_consts(e);

@@ -296,15 +296,16 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         eta2 = fmaf(f * f, weta2[w], eta2);
     }
     FSTAMP(3);
-    bool xlate = false;   // the peer exchange timed out: this step keeps the warm start (w_eps = 0)
+    bool xlate = false;   // the peer exchange gave the step up: this step keeps the warm start (w_eps = 0)
     if (xpeers != nullptr && mode != 1) {
         // Peer exchange (sharded V == 1 engines, mppi_dev.h kXW): this block's partial goes to every
         // other rank's region (a FINAL only; READBACK re-reads the last step's), then the other
         // ranks' partials of this block come back from this rank's region, each 8 B word valid once
-        // its tag is this step's, and all are combined in rank order (the same order on every rank: every rank finalises
-        // bit-identically; one rank reproduces the unsharded step exactly, f = exp(0) = 1).
+        // its tag is this step's, and all are combined in rank order (the same order on every rank:
+        // every rank finalises bit-identically; one rank reproduces the unsharded step exactly,
+        // f = exp(0) = 1).
         const uint32_t step = __builtin_amdgcn_readfirstlane(xstep);
-        const uint32_t tag = peer_tag(step, __builtin_amdgcn_readfirstlane(xep)), atag = tag | kTagAbort;
+        const uint32_t tag = peer_tag(step, __builtin_amdgcn_readfirstlane(xep));
         // (the grid from geo, not gridDim: that reads the hidden kernel arguments, which native
         // dispatch does not supply; V == 1 on a peer-exchange engine)
         const size_t nbk = (size_t)8 * na * ts, blk = blockIdx.x;
@@ -316,7 +317,19 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             return (gst64*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(xpl >> 32), d) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)xpl, d));
         };
+        typedef __attribute__((address_space(1))) unsigned long long gu64;
+        gu64* const ctl = (gu64*)xlocal - kXCtl;   // the ranks' timeout reports, the decision words
         if (mode == 0) {   // (this rank's own partial stays in registers: no round trip through memory)
+            if (uint32_t* xs = T.xstall) {   // diagnostics (mppi_debug_peer_stall): one block's stores late
+                const uint32_t sv = ld_dev(xs);
+                if (sv != 0u && (sv & 0xFFFFu) == (uint32_t)blk) {
+                    const uint64_t t_s = __builtin_amdgcn_s_memrealtime(), ticks = (uint64_t)(sv >> 16) * 100000ull;
+                    while (__builtin_amdgcn_s_memrealtime() - t_s < ticks) __builtin_amdgcn_s_sleep(127);
+                    if (lane == 0) __hip_atomic_store(xs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // once
+                }
+            }
+            if (blk == 0 && lane == 0)   // the previous step's decision word (see mppi_dev.h kXDec)
+                __hip_atomic_store(ctl + kXDec + (par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
             const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
 #pragma unroll
@@ -339,74 +352,92 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         // the loads issued per rank behind divergent branches, the compiler waited for each load
         // before the next: 2 (G - 1) serial round trips per round, ~14 at G = 8.)  Which ranks are
         // still pending is wave-uniform: a rank is done when every lane that needs a word of it has
-        // seen the step's tag (a ballot), and its words are taken from that round.
-        typedef __attribute__((address_space(1))) unsigned long long gu64;
+        // seen the step's tag (a ballot), and its words are taken from that round.  true: given up
+        // (the bound passed or, heeding reports, some rank reported a timeout since the last reset).
         const bool needc = lane < W, needh = lane < kHdr;
         uint32_t pend = ((1u << xn) - 1u) & ~(1u << xme);   // (uniform)
         const unsigned long long* src = xlocal + (par * (size_t)xn * nbk + blk) * kXW;
-        gu64* const ctl = (gu64*)xlocal - kXCtl;   // the ranks' timeout reports (mppi_dev.h kXCtl)
-        const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
-        bool late = false;
-        while (pend != 0u) {
-            unsigned long long xc[kMaxPeers], xh[kMaxPeers];
+        auto poll = [&](bool heed_reports) -> bool {
+            const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+            while (pend != 0u) {
+                unsigned long long xc[kMaxPeers], xh[kMaxPeers];
 #pragma unroll
-            for (int r = 0; r < kMaxPeers; ++r) {
-                xc[r] = 0ull; xh[r] = 0ull;
-                if ((pend >> r) & 1u) {   // (uniform branch)
-                    gu64* s = (gu64*)(src + (size_t)r * nbk * kXW);
-                    // lane < 64 <= kXW - kHdr: every lane's word lies inside the rank's slot (the
-                    // words past W are not written and not checked)
-                    xc[r] = __hip_atomic_load(s + kHdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    xh[r] = __hip_atomic_load(s + (lane & (kHdr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                for (int r = 0; r < kMaxPeers; ++r) {
+                    xc[r] = 0ull; xh[r] = 0ull;
+                    if ((pend >> r) & 1u) {   // (uniform branch)
+                        gu64* s = (gu64*)(src + (size_t)r * nbk * kXW);
+                        // lane < 64 <= kXW - kHdr: every lane's word lies inside the rank's slot (the
+                        // words past W are not written and not checked)
+                        xc[r] = __hip_atomic_load(s + kHdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        xh[r] = __hip_atomic_load(s + (lane & (kHdr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+                if (heed_reports) {   // (in the same batch of loads: lane r < xn reads rank r's report)
+                    const unsigned long long xk = __hip_atomic_load(ctl + (lane < xn ? lane : 0), __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (__builtin_amdgcn_ballot_w64(lane < xn && xk != 0ull) != 0ull) return true;
+                }
+#pragma unroll
+                for (int r = 0; r < kMaxPeers; ++r) {
+                    if (!((pend >> r) & 1u)) continue;
+                    const bool ok = (!needc || (uint32_t)(xc[r] >> 32) == tag) && (!needh || (uint32_t)(xh[r] >> 32) == tag);
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {
+                        nv[r] = needc ? __uint_as_float((uint32_t)xc[r]) : 0.0f;
+                        hv[r] = needh ? __uint_as_float((uint32_t)xh[r]) : 0.0f;
+                        pend &= ~(1u << r);
+                    }
+                }
+                pend = __builtin_amdgcn_readfirstlane(pend);
+                if (pend == 0u) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_in > kPeerWaitTicks) return true;   // (2 s)
+                __builtin_amdgcn_s_sleep(1);
+            }
+            return false;
+        };
+        bool late = poll(true), torn = false;
+        if (mode == 0) {
+            // One decision per rank and step (mppi_dev.h kXDec): the first block's proposal, adopted
+            // by every block before any of them writes its slice of u_prev.
+            unsigned long long dec = 0ull;
+            if (lane == 0) {
+                gu64* dw = ctl + kXDec + par;
+                const unsigned long long mine = ((unsigned long long)tag << 32) | (late ? kDecGiveUp : kDecCommit);
+                unsigned long long cur = 0ull;
+                for (;;) {   // cur: the word as the swap found it
+                    if (__hip_atomic_compare_exchange_strong(dw, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT)) { dec = mine; break; }
+                    if ((uint32_t)(cur >> 32) == tag) { dec = cur; break; }   // decided by another block
+                    // (else an earlier step's word, left by a counter rewind: replace it)
                 }
             }
-            // (in the same batch of loads: lane r < xn reads rank r's timeout report)
-            const unsigned long long xk = __hip_atomic_load(ctl + (lane < xn ? lane : 0), __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_SYSTEM);
-            // Any rank reported a timeout since the last reset, or a pending peer gave this very step
-            // up (its header words carry the step's abort tag): this step is given up too, at once.
-            // After one rank's timeout every rank keeps its warm start until the host resets the
-            // exchange, so no rank goes on updating a warm start the others did not.
-            uint64_t bad = __builtin_amdgcn_ballot_w64(lane < xn && xk != 0ull);
+            const bool commit = ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dec) & 3u) == kDecCommit;
+            if (late && commit) {        // another block of this rank has updated its slice: complete
+                late = poll(false);      // (a second bound; the peers' words stay in place, reports aside)
+                torn = late;
+            } else if (!late && !commit) {
+                late = true;             // the rank gave the step up: keep this slice too
+            }
+            if (late && (torn || !commit)) {
+                // Give the step up on every rank: this rank's timeout report into every rank's region
+                // (its own included) -- a peer still polling this step gives it up at once -- and the
+                // sticky word the host reads (mppi_synchronize / mppi_read_outputs / mppi_peer_status);
+                // a torn rank also its torn word (the resync's source is a rank that is not torn).
+                const unsigned long long cw = ((unsigned long long)tag << 32) | 1ull;
 #pragma unroll
-            for (int r = 0; r < kMaxPeers; ++r)
-                if ((pend >> r) & 1u) bad |= __builtin_amdgcn_ballot_w64(needh && (uint32_t)(xh[r] >> 32) == atag);
-            if (bad != 0ull) { late = true; break; }
-#pragma unroll
-            for (int r = 0; r < kMaxPeers; ++r) {
-                if (!((pend >> r) & 1u)) continue;
-                const bool ok = (!needc || (uint32_t)(xc[r] >> 32) == tag) && (!needh || (uint32_t)(xh[r] >> 32) == tag);
-                if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {
-                    nv[r] = needc ? __uint_as_float((uint32_t)xc[r]) : 0.0f;
-                    hv[r] = needh ? __uint_as_float((uint32_t)xh[r]) : 0.0f;
-                    pend &= ~(1u << r);
+                for (int d = 0; d < kMaxPeers; ++d) {
+                    if (d >= xn) continue;
+                    gst64* rg = region(d);
+                    if (lane == 0) __hip_atomic_store(rg - kXCtl + xme, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                uint32_t* xe = T.xerr;   // (read only here: the late path)
+                if (lane == 0 && xe) {
+                    __hip_atomic_store(xe, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (torn) __hip_atomic_store(xe + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
-            pend = __builtin_amdgcn_readfirstlane(pend);
-            if (pend == 0u) break;
-            if (__builtin_amdgcn_s_memrealtime() - t_in > kPeerWaitTicks) { late = true; break; }   // (2 s)
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (late && mode == 0) {
-            // Give the step up on every rank: this rank's timeout report into every rank's region
-            // (its own included), the step's abort tag over this block's header words in the peers'
-            // regions (a peer still polling this step gives it up too, instead of updating alone),
-            // and the sticky word the host reads (mppi_synchronize / mppi_read_outputs / mppi_peer_status).
-            const unsigned long long cw = ((unsigned long long)tag << 32) | 1ull;
-            const unsigned long long aw = (unsigned long long)atag << 32;
-#pragma unroll
-            for (int d = 0; d < kMaxPeers; ++d) {
-                if (d >= xn) continue;
-                gst64* rg = region(d);
-                if (lane == 0) __hip_atomic_store(rg - kXCtl + xme, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (d != xme && lane < kHdr)
-                    __hip_atomic_store(rg + off + lane, aw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            uint32_t* xe = T.xerr;   // (read only here: the late path)
-            if (lane == 0 && xe) __hip_atomic_store(xe, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         rho = INFINITY;
-        nanf = late ? 2.0f : 0.0f;
+        nanf = late ? (torn ? 3.0f : 2.0f) : 0.0f;   // (the records' nan flag: 2 given up, 3 torn)
 #pragma unroll
         for (int r = 0; r < kMaxPeers; ++r) {
             if (r < xn) {

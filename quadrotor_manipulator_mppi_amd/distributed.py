@@ -235,6 +235,12 @@ class ShardedEngine:
         self.buf: Optional[torch.Tensor] = None
         self.native_error: Optional[str] = None
         self.resyncs = 0   # peer-exchange recoveries (resync) so far
+        # On a multi-rank peer exchange the ranks agree on a timeout (a collective) every
+        # ``agree_every`` control calls of ``step`` and in every ``synchronize``; in between a step
+        # is collective-free (a timeout is rank-wide on the device already: the other ranks' steps
+        # are given up too, warm starts held, until the agreement resyncs them).  1 = every call.
+        self.agree_every = max(1, int(os.environ.get("MPPI_PEER_AGREE_EVERY", "100")))
+        self._calls = 0
 
         def fresh_engine():
             self.engine.close()
@@ -290,10 +296,12 @@ class ShardedEngine:
                 self.step_async()
 
     def step(self, state, d_noise_ptr: int = 0):
-        """One control step -> (out, u0, [StepStats]).  On a multi-rank peer exchange it is a
-        collective: the ranks agree on whether any of them gave the step up (one MAX all-reduce)
-        and, if so, resynchronise (``resync``) before returning, every rank reporting
-        ``exchange_timeout``."""
+        """One control step -> (out, u0, [StepStats]).  A step given up by the peer exchange reports
+        ``exchange_timeout`` (and ``nonfinite``) on this rank at once; on a multi-rank peer exchange
+        every ``agree_every``-th call is also a collective -- the ranks agree on whether any of them
+        gave a step up since the last agreement (one MAX all-reduce of the sticky word) and, if so,
+        resynchronise (``resync``), every rank then reporting ``exchange_timeout``.  Every rank must
+        make the same calls (the control loop runs in lockstep on the ranks)."""
         if (self.world == 1 or self.mode in ("peer", "vehicles")) and not d_noise_ptr:   # one C call, as the drop-in classes step
             out, u0, st = self.engine.step(state)
         else:
@@ -301,12 +309,14 @@ class ShardedEngine:
             self.step_async(d_noise_ptr)
             out, u0, st = self.engine.read_outputs()
         if self._checks_exchange():
-            local = any(s.exchange_timeout for s in st)
-            if _any_rank(local, self.group, self.local):
-                self.resync()
-                for s in st:
-                    s.exchange_timeout = True
-                    s.nonfinite = True
+            self._calls += 1
+            if self._calls % self.agree_every == 0:
+                local = any(s.exchange_timeout for s in st) or self.engine.peer_status(reports=False)[0] != 0
+                if _any_rank(local, self.group, self.local):
+                    self.resync()
+                    for s in st:
+                        s.exchange_timeout = True
+                        s.nonfinite = True
         return out, u0, st
 
     # ------------------------------------------------------------- failure handling (peer)
@@ -336,7 +346,8 @@ class ShardedEngine:
 
     def resync(self):
         """Collective recovery after a peer-exchange timeout (every rank calls it): every rank takes
-        rank 0's warm start u_prev and step counter and a fresh exchange epoch, and its exchange
+        the warm start u_prev and step counter of the lowest rank whose warm start is not torn
+        (rank 0 normally) and a fresh exchange epoch, and its exchange
         region is cleared between two barriers (no kernel writes into any region while it is
         cleared, and no rank steps before every region is clear).  Afterwards the ranks' warm starts
         are bit-identical and the exchange runs again (the sharded reduction is
@@ -351,7 +362,15 @@ class ShardedEngine:
         u = torch.from_numpy(eng.get_u_prev()).to(dev)
         _, _, epoch = eng.peer_status(reports=False)
         ctl = torch.tensor([eng.get_step_counter(), epoch], dtype=torch.int64, device=dev)
-        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        # the source: the lowest rank whose warm start is not torn (mppi_peer_info; a step's blocks
+        # all update or all keep their slices unless a peer stayed silent through two bounds)
+        torn = bool(eng.peer_info()[2])
+        first = torch.tensor([self.world if torn else self.rank], dtype=torch.int64, device=dev)
+        dist.all_reduce(first, op=dist.ReduceOp.MIN, group=self.group)
+        g0 = int(first.item())
+        g0 = 0 if g0 >= self.world else g0   # (every rank torn: rank 0's, as before)
+        self.resync_source = g0
+        src = dist.get_global_rank(self.group, g0) if self.group is not None else g0
         dist.broadcast(u, src=src, group=self.group)
         dist.broadcast(ctl, src=src, group=self.group)
         step, epoch = (int(x) for x in ctl.tolist())

@@ -254,6 +254,15 @@ class Engine:
         capi.check(self._L.mppi_peer_status(self._h, C.byref(st), rep, C.byref(ep)), "peer_status")
         return st.value, (list(rep) if reports else None), ep.value
 
+    def peer_info(self):
+        """(connected, rank, torn) of the peer exchange (mppi_peer_info): ``connected`` = the ranks whose
+        word reached this rank's region in the connection probe's kernel phase, ``rank`` = this
+        engine's shard rank, ``torn`` = the step tag of a step this rank's warm start came out of torn
+        (some slices updated, others kept; 0 = none)."""
+        n, r, t = C.c_int32(0), C.c_int32(0), C.c_uint32(0)
+        capi.check(self._L.mppi_peer_info(self._h, C.byref(n), C.byref(r), C.byref(t)), "peer_info")
+        return n.value, r.value, t.value
+
     def peer_reset(self, step: int, epoch: int):
         """Clear this rank's region and sticky word, take the agreed step counter and epoch
         (collective recovery: every rank synchronised, a barrier before and after)."""

@@ -3,6 +3,7 @@ are built from the measurements the way a torchrun launch builds them.  Two gloo
 stand in for two GPUs: each reports its own batch times and kernel times, ``reduce_max``
 takes the max over ranks, and rank 0 builds the line with ``make_line``."""
 import argparse
+import json
 import os
 import socket
 
@@ -130,3 +131,86 @@ def test_primary_weak_and_c4_secondary_at_two_ranks():
     assert e["n_gpus"] == 2 and e["scaling"] == "strong" and e["samples_total"] == 65536
     assert e["value"] == pytest.approx(65536 * 64 / (s["dt"] / 20))
     assert e["rollout_us_max_over_ranks"] == 13.6 and e["exchange"] == "torch"
+
+
+# ------------------------------------------------------------ bench.py --gpus N without a launcher
+_STUB = r"""
+import json, os, sys
+rank = int(os.environ.get("RANK", "0"))
+print("a rank's stray stdout line", flush=True)
+if rank == 0:
+    print(json.dumps({"metric": "m", "value": 1.0, "argv": sys.argv[1:],
+                      "world": os.environ.get("WORLD_SIZE"), "spawned": os.environ.get("MPPI_BENCH_SPAWNED")}),
+          flush=True)
+sys.exit(int(os.environ.get("STUB_RC", "0")))
+"""
+
+
+def test_spawn_ranks_relays_one_line_and_the_child_rc(tmp_path, capsys):
+    """``bench.py --gpus N`` without WORLD_SIZE runs the ranks as a CHILD
+    (spawn_ranks) and relays exactly one bench line -- rank 0's; other stdout lines go to stderr --
+    and returns the child's exit code.  Stub child: a script that prints what it was given."""
+    import io
+    import sys
+    stub = tmp_path / "stub.py"
+    stub.write_text(_STUB)
+    for rc in (0, 3):
+        out = io.StringIO()
+        env_rc = {"STUB_RC": str(rc)}
+        os.environ.update(env_rc)
+        try:
+            got = bench.spawn_ranks([sys.executable, str(stub), "--gpus", "2", "--steps", "7"], out=out)
+        finally:
+            del os.environ["STUB_RC"]
+        lines = [ln for ln in out.getvalue().splitlines() if ln.strip()]
+        assert got == rc and len(lines) == 1, (got, lines)
+        d = json.loads(lines[0])
+        assert d["argv"] == ["--gpus", "2", "--steps", "7"] and d["spawned"] == "1"
+    assert "stray stdout line" in capsys.readouterr().err
+    # a child that prints no bench line and exits 0 is a failure, not a silent empty run
+    quiet = tmp_path / "quiet.py"
+    quiet.write_text("print('nothing to relay')\n")
+    out = io.StringIO()
+    assert bench.spawn_ranks([sys.executable, str(quiet)], out=out) == 1 and out.getvalue() == ""
+
+
+def test_spawn_through_torch_distributed_run(tmp_path):
+    """The launcher command itself (torch.distributed.run, static rendezvous on 127.0.0.1): two ranks
+    of a stub, every argument forwarded after the script, WORLD_SIZE = 2 in the ranks, rank 0's line
+    relayed alone, the launcher's exit code returned."""
+    import io
+    stub = tmp_path / "stub.py"
+    stub.write_text(_STUB)
+    argv = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--secondary", ""]
+    cmd = bench.launcher_cmd(2, argv, script=str(stub))
+    assert cmd[cmd.index(str(stub)) + 1:] == argv and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert bench.launcher_cmd(8, argv)[-len(argv) - 1] == os.path.abspath(bench.__file__)
+    out = io.StringIO()
+    rc = bench.spawn_ranks(cmd, out=out)
+    lines = [ln for ln in out.getvalue().splitlines() if ln.strip()]
+    assert rc == 0 and len(lines) == 1, (rc, lines)
+    d = json.loads(lines[0])
+    assert d["argv"] == argv and d["world"] == "2"
+
+
+def test_main_spawns_without_a_launcher(monkeypatch):
+    """main() with --gpus 2 and no WORLD_SIZE goes to spawn_ranks with its own argv, before any GPU
+    call, and exits with the child's code; under a launcher (WORLD_SIZE set) it never spawns."""
+    import sys
+    seen = {}
+
+    def fake_spawn(cmd, out=None):
+        seen["cmd"] = cmd
+        return 5
+    monkeypatch.setattr(bench, "spawn_ranks", fake_spawn)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("MPPI_BENCH_SPAWNED", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "9"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 5
+    assert seen["cmd"][-4:] == ["--gpus", "2", "--steps", "9"] and "--nproc-per-node=2" in seen["cmd"]
+    monkeypatch.setenv("MPPI_BENCH_SPAWNED", "1")
+    with pytest.raises(SystemExit, match="own launcher"):
+        bench.main()

@@ -419,10 +419,11 @@ def test_gloo_world2_vehicle_split_equals_one_fleet():
 class _FakeTimeoutEngine:
     """The engine calls ShardedEngine.synchronize / resync make, on the host only (no GPU here):
     rank ``late`` reports a timeout (mppi_synchronize's MPPI_ERR_PEER_TIMEOUT) until reset."""
-    def __init__(self, rank, late):
+    def __init__(self, rank, late, torn=None):
         from quadrotor_manipulator_mppi_amd import _capi
         self._exc = _capi.PeerTimeout
         self.timed_out = rank == late
+        self.rank, self.torn = rank, (0x80000007 if rank == torn else 0)
         self.u = np.full((1, 4, 3), float(rank + 1), np.float32)
         self.ctr, self.epoch = 10 + rank, 3 + rank
         self.resets = []
@@ -443,24 +444,52 @@ class _FakeTimeoutEngine:
     def peer_status(self, reports=True):
         return (1 if self.timed_out else 0), None, self.epoch
 
+    def peer_info(self):
+        return 2, self.rank, self.torn
+
+    def step(self, state):   # (the control call: its stats report this rank's sticky word)
+        from quadrotor_manipulator_mppi_amd.engine import StepStats
+        return None, None, [StepStats(0.0, 1.0, 1.0, self.timed_out, False, self.timed_out)]
+
     def peer_reset(self, step, epoch):
         self.timed_out = False
+        self.torn = 0
         self.ctr, self.epoch = step, epoch
         self.resets.append((step, epoch))
 
 
-def _agree_main(rank, world, port, late, q):
+def _fake_sharded(rank, world, late, torn=None, agree_every=100):
+    from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
+    se = object.__new__(ShardedEngine)   # (the host protocol only: no Engine, no HIP stream)
+    se.group, se.rank, se.world, se.local, se.mode, se.resyncs = None, rank, world, 0, "peer", 0
+    se.agree_every, se._calls = agree_every, 0
+    se.engine = _FakeTimeoutEngine(rank, late, torn)
+    return se
+
+
+def _agree_main(rank, world, port, late, q, torn=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
-        se = object.__new__(ShardedEngine)   # (the host protocol only: no Engine, no HIP stream)
-        se.group, se.rank, se.world, se.local, se.mode, se.resyncs = None, rank, world, 0, "peer", 0
-        se.engine = _FakeTimeoutEngine(rank, late)
+        se = _fake_sharded(rank, world, late, torn)
         first = se.synchronize()
         second = se.synchronize()
         e = se.engine
         q.put((rank, first, second, e.u, e.ctr, e.epoch, e.resets, se.resyncs))
+    finally:
+        dist.destroy_process_group()
+
+
+def _step_agree_main(rank, world, port, late, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        se = _fake_sharded(rank, world, late, agree_every=3)
+        seen = []
+        for _ in range(6):   # calls 3 and 6 are the agreements (collectives); 1, 2, 4, 5 are local
+            st = se.step(None)[2]
+            seen.append((bool(st[0].exchange_timeout), se.resyncs))
+        q.put((rank, seen, se.engine.u))
     finally:
         dist.destroy_process_group()
 
@@ -490,3 +519,44 @@ def test_gloo_world2_peer_timeout_agreement_and_resync(late):
         assert first is True and second is False and n == 1, (rank, first, second, n)
         assert np.array_equal(u, np.full((1, 4, 3), 1.0, np.float32)), "rank 0's warm start on every rank"
         assert (ctr, epoch) == (10, 4) and resets == [(10, 4)]
+
+
+def _run2(target, *args):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _agree_torn_main(rank, world, port, q):
+    _agree_main(rank, world, port, 0, q, torn=0)
+
+
+def test_gloo_world2_resync_source_skips_a_torn_rank():
+    """A rank whose warm start came out of a step torn (mppi_peer_info: a finalize block that timed
+    out twice while the rank's other blocks had updated their slices) is not the resync's source:
+    the lowest rank that is not torn is (rank 1 here), so every rank ends with a whole warm start."""
+    res = _run2(_agree_torn_main)
+    for rank, first, second, u, ctr, epoch, resets, n in res:
+        assert first is True and n == 1
+        assert np.array_equal(u, np.full((1, 4, 3), 2.0, np.float32)), "rank 1's warm start on every rank"
+        assert (ctr, epoch) == (11, 5) and resets == [(11, 5)]
+
+
+def test_gloo_world2_step_agrees_every_n_calls():
+    """ShardedEngine.step keeps the control call collective-free between agreements: a
+    rank whose step was given up reports it at once on that rank, and the ranks agree (and resync)
+    only on every ``agree_every``-th call -- here the 3rd -- on every rank alike."""
+    res = _run2(_step_agree_main, 1)
+    r0, r1 = res[0][1], res[1][1]
+    assert r0 == [(False, 0), (False, 0), (True, 1), (False, 1), (False, 1), (False, 1)], r0
+    assert r1 == [(True, 0), (True, 0), (True, 1), (False, 1), (False, 1), (False, 1)], r1
+    assert np.array_equal(res[0][2], res[1][2])

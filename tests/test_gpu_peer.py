@@ -487,3 +487,84 @@ def test_peer_in_process_ranks_equal_one_engine(G):
     finally:
         for e in ranks:
             e.close()
+
+
+def _stall(e, block, ms):
+    """mppi_debug_peer_stall: the next FINAL's finalize block ``block`` stores its partial ``ms`` late."""
+    import ctypes as C
+    from quadrotor_manipulator_mppi_amd import _capi
+    fn = _capi.lib().mppi_debug_peer_stall
+    fn.restype, fn.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_int32]
+    _capi.check(fn(e._h, block, ms), "debug_peer_stall")
+
+
+# block 3 of the whole-body finalize grid (8 XCD lanes x 2 dim groups x 8 t-slices) is dim 3,
+# t-slice 0 (t in [0, 8), the slice that also writes the dim's outputs): csrc/mppi_finalize.hip
+STALL_BLOCK, STALL_DIM, STALL_T = 3, 3, slice(0, 8)
+
+
+@pytest.mark.parametrize("stall_ms", [3000, 5000])
+def test_peer_one_block_stalled_all_or_nothing(stall_ms):
+    """ONE finalize block of rank 1 stores its partial ``stall_ms`` late (every
+    other block of the step on time), so rank 0's matching block passes its 2 s bound while rank 0's
+    other blocks have already updated their slices of u_prev.  Within a rank the step is all or
+    nothing (mppi_dev.h kXDec: one decision per rank and step, a compare-and-swap before any slice is
+    written): rank 0's late block finds its rank committed and keeps polling for a second bound.
+    3000 ms: the partial arrives within it -- both ranks end FULLY UPDATED, bit-identical to a pair
+    that never stalled, and no rank reports anything.  5000 ms: two bounds pass -- rank 0's warm start
+    is torn (that slice kept), which it reports (torn word, timeout report, nan flag 3) instead of
+    leaving silently; rank 1 completes (its late block finds its rank committed, the words are in
+    place) and is fully updated; the resync takes rank 1's warm start (the lowest rank not torn),
+    after which both ranks equal the never-stalled pair and step on bit-identically."""
+    ref, pair = _pair(), _pair()
+    try:
+        for p in (ref, pair):
+            for e in p:
+                e.run_steps(3)
+            assert _sync_all(p) == [False, False]
+        held = pair[0].get_u_prev()
+        assert np.array_equal(held, ref[0].get_u_prev())
+        for e in ref:
+            e.run_steps(1)
+        assert _sync_all(ref) == [False, False]
+        want = ref[0].get_u_prev()
+        assert not np.array_equal(want, held)
+        _stall(pair[1], STALL_BLOCK, stall_ms)
+        for e in pair:
+            e.run_steps(1)
+        timed = _sync_all(pair)
+        u = [e.get_u_prev() for e in pair]
+        torn = [e.peer_info()[2] for e in pair]
+        assert [e.peer_info()[:2] for e in pair] == [(2, 0), (2, 1)], "both ranks connected"
+        assert np.array_equal(u[1], want), "rank 1 fully updated"
+        if stall_ms < 4000:
+            assert timed == [False, False] and torn == [0, 0], (timed, torn)
+            assert np.array_equal(u[0], want), "rank 0 fully updated (its late block completed)"
+            for e in pair:
+                _, _, st = e.read_outputs()
+                assert not st[0].nonfinite and not st[0].exchange_timeout
+        else:
+            assert timed[0] and torn[0] != 0 and torn[1] == 0, (timed, torn)
+            exp = want.copy()
+            exp[0, STALL_T, STALL_DIM] = held[0, STALL_T, STALL_DIM]
+            assert np.array_equal(u[0], exp), "rank 0: exactly the stalled block's slice kept, reported torn"
+            # the resync (ShardedEngine.resync's choice, in process): the lowest rank that is not torn
+            src = min(r for r in range(2) if not torn[r])
+            assert src == 1
+            _sync_all(pair)
+            u_src, step = pair[src].get_u_prev(), pair[src].get_step_counter()
+            epoch = max(e.peer_status(reports=False)[2] for e in pair)
+            for e in pair:
+                e.peer_reset(step, epoch + 1)
+            for e in pair:
+                e.set_u_prev(u_src)
+            assert [e.peer_info()[2] for e in pair] == [0, 0]
+            assert all(np.array_equal(e.get_u_prev(), want) for e in pair), "whole warm starts after the resync"
+        for p in (ref, pair):   # and stepping on: bit-identical to the pair that never stalled
+            for e in p:
+                e.run_steps(5)
+            assert _sync_all(p) == [False, False]
+        assert all(np.array_equal(e.get_u_prev(), ref[0].get_u_prev()) for e in pair + ref[1:])
+    finally:
+        for e in ref + pair:
+            e.close()
