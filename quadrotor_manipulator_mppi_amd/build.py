@@ -57,6 +57,13 @@ def code_object_path(lib: str, unit: str) -> str:
 
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 EXTRA = os.environ.get("MPPI_HIPCC_EXTRA", "").split()   # experiment flags (tools/), empty in production
+# every environment knob that changes the flags of some unit (experiments only); BUILD_INFO.json records
+# the ones set, and the production library refuses them (build one elsewhere with MPPI_BUILD_OUT)
+KNOBS = ("MPPI_HIPCC_EXTRA", "MPPI_C3_SCHED", "MPPI_C3_EXTRA", "MPPI_MAXILP_UNITS", "MPPI_OFFLOAD_ARCH")
+
+
+def knobs_set() -> dict:
+    return {k: os.environ[k] for k in KNOBS if os.environ.get(k)}
 
 
 def hipcc() -> str:
@@ -80,6 +87,9 @@ def _stale() -> bool:
 def build(force: bool = False, debug: bool = False, verbose: bool = False, stamps: bool = False,
           asan: bool = False) -> str:
     out = os.environ.get("MPPI_BUILD_OUT") or (LIB_STAMPS if stamps else LIB_ASAN if asan else LIB)
+    if os.path.abspath(out) == os.path.abspath(LIB) and knobs_set():
+        raise RuntimeError(f"experiment build knobs {sorted(knobs_set())} set for the production library "
+                           f"{LIB}: unset them, or build elsewhere with MPPI_BUILD_OUT")
     if not force and not stamps and not asan and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
@@ -141,6 +151,7 @@ def _write_build_info(out: str) -> None:
     except (OSError, subprocess.SubprocessError):
         pass
     info = {"library": os.path.basename(out), "git_head": head, "arch": ARCH, "extra_flags": EXTRA,
+            "knobs": knobs_set(),
             "built_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
     if out == LIB:
         with open(os.path.join(LIB_DIR, "BUILD_INFO.json"), "w") as f:
