@@ -398,6 +398,10 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         w["n_samples"] //= world
     native = force_native if force_native is not None else (
         None if os.environ.get("MPPI_NATIVE_COMM", "1") != "0" else False)
+    if native is None and world > 1:
+        # the engine-owned exchange (peer, else RCCL, else the torch collective) over any process group:
+        # a rehearsal's gloo group carries the peer exchange's handle all-gather just as RCCL's would
+        native = True
     se = ShardedEngine(seed=1234, native=native, mode=mode, **w)
     eng = se.engine
     V = eng.V   # this rank's vehicles (the fleet-wide ones: se.vehicles)

@@ -37,6 +37,7 @@ def load(path):
 def main():
     reps = int(sys.argv[1])
     runs = [r.split() for r in sys.argv[2].split(";") if r.strip()]
+    # (the engines below index the runs by position; "peer" is stripped per run there)
     libs = sys.argv[3:]
     steps = int(os.environ.get("MPPI_AB_STEPS", "500"))
     ncalls = int(os.environ.get("MPPI_AB_CALLS", "20"))   # 0 for builds without completion flags (knockouts)
@@ -48,9 +49,15 @@ def main():
         os.environ.update(env)
         capi._lib = load(p)
         for ri, r in enumerate(runs):
+            peer = "peer" in r   # "<model K H peer>": one rank exchanging with itself (the C4 rank's step)
+            r = [x for x in r if x != "peer"]
             model, K, H = r[0], int(r[1]), int(r[2])
             V = int(r[3]) if len(r) > 3 else 1
             e = Engine(make_config(model, n_samples=K, n_horizon=H, n_vehicles=V, state_f64=(model == "arm")))
+            if peer:
+                e.peer_connect([e.peer_open()])
+                for ph in (0, 1, 2):
+                    e.peer_probe(ph)
             for v in range(V):
                 if model in ("drone", "quadrotor"):
                     e.set_target([1.0, 2.0, 3.4], vehicle=v)
