@@ -311,11 +311,12 @@ mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports
 /* The connection and the warm start's integrity (ABI 9): connected = the ranks whose tagged word
  * reached this rank's region in mppi_peer_probe's kernel phase (phase 2; 0 before it), rank = this
  * engine's shard_rank, torn (may be NULL) = the step tag of a step this rank's warm start came out
- * of torn, 0 = none.  Within a rank a step is all or nothing: its finalize blocks decide once,
- * through a compare-and-swap in the rank's own region, whether every block updates its slice of
- * u_prev or every block keeps it; a block that timed out on a rank whose other blocks already
- * updated keeps polling for a second 2 s bound, and only if that passes too is the warm start torn
- * (the resync then takes its u_prev from a rank that is not torn). */
+ * of torn, 0 = none.  Within a rank a step is all or nothing: a finalize block updates its slice
+ * of u_prev only if every peer word arrived in time with no timeout report in sight, and marks the
+ * rank's decision word; a late block reports, waits 100 us for any such mark, and if its rank
+ * committed keeps polling for a second 2 s bound instead of keeping its slice.  Only if that
+ * passes too is the warm start torn (the resync then takes its u_prev from a rank that is not
+ * torn). */
 mppi_status mppi_peer_info(mppi_engine* e, int32_t* connected, int32_t* rank, uint32_t* torn);
 /* Collective recovery after a timeout: with every rank's engine synchronised and a barrier passed
  * (no kernel writes into any region), clear this rank's region and sticky word and take the step

@@ -476,7 +476,7 @@ static void load_fences() {
 static const int kScope[3] = {HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_AGENT, HSA_FENCE_SCOPE_SYSTEM};
 
 static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l, void* args, hsa_signal_t sig,
-                       int acquire, int release) {
+                       int acquire, int release, bool barrier = true) {
     const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
     while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
     auto* p = (hsa_kernel_dispatch_packet_t*)q->base_address + (idx & (q->size - 1));
@@ -496,7 +496,7 @@ static inline void put(hsa_queue_t* q, const Kern& k, const mppi::LaunchDesc& l,
     // each kernel waits for the one before (barrier bit) and sees its writes (agent-scope
     // acquire); the batch's last one releases to system scope (the outputs in host memory)
     const uint16_t header =
-        (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1 << HSA_PACKET_HEADER_BARRIER) |
+        (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
                    (kScope[acquire] << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                    (kScope[release] << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
     const uint32_t setup = 3u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
@@ -568,7 +568,7 @@ static bool probe_dispatch_ids(Step* s, std::string* why) {
 
 std::unique_lock<std::recursive_mutex> step_guard(Step* s) { return std::unique_lock<std::recursive_mutex>(s->mu); }
 
-int step_dispatch(Step* s, int n, std::string* err) {
+int step_dispatch(Step* s, int n, std::string* err, bool overlap) {
     std::lock_guard<std::recursive_mutex> qlk(s->mu);
     if (!s->valid) { *err = "step_dispatch before step_prepare"; return -1; }
     if (n <= 0) return 0;
@@ -581,7 +581,8 @@ int step_dispatch(Step* s, int n, std::string* err) {
     load_fences();
     for (int i = 0; i < n; ++i) {
         const bool last = i == n - 1;
-        put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1]);
+        put(s->q, s->kr, s->roll, ra, none, i == 0 ? std::max(1, g_fence[0]) : g_fence[0], g_fence[1],
+            !(overlap && i > 0));
         put(s->q, s->kf, s->fin, fa, last ? s->done : none, g_fence[2], last ? 2 : g_fence[3]);
         // the doorbell takes the index of the last packet written
         hsa_signal_store_screlease(s->q->doorbell_signal, (hsa_signal_value_t)hsa_queue_load_write_index_relaxed(s->q) - 1);

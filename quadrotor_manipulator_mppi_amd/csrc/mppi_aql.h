@@ -39,7 +39,9 @@ int step_prepare(Step* s, const mppi::LaunchDesc& roll, const mppi::LaunchDesc& 
                  uint32_t step_off, std::string* err);
 // n (rollout, finalize) pairs, each kernel dependent on the one before; the last finalize
 // carries the completion signal and a system-scope release.
-int step_dispatch(Step* s, int n, std::string* err);
+// overlap: every rollout after the first without the barrier bit (it starts while the finalize
+// before it runs and waits for it in the kernel: mppi_device.h kNoiseOverlap)
+int step_dispatch(Step* s, int n, std::string* err, bool overlap = false);
 // The queue held against other threads' packets (the prewarm thread's step_touch) while the
 // guard lives: a step_prepare and the step_dispatch after it must see the same packet index,
 // or the batch's rollouts would run later steps than prepared.

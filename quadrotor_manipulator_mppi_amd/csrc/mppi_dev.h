@@ -125,6 +125,10 @@ struct DevParams {
     float q_g;                    // gravity magnitude, g = (0, 0, -q_g)
     int32_t q_literal_jinv;       // t >= 1 applies inv(J) to the body rates, as the commented loop
                                   // (drone_mppi.py:73-76); 0 = J at every step
+    // overlapped native batches (kNoiseOverlap, MPPI_OVERLAP=1): the finalize blocks' step counters,
+    // (V, A, ts) words each incremented once per FINAL (FinTail::xovl), and their count per vehicle
+    const uint32_t* ovl;
+    int32_t ovl_n;
 };
 constexpr int kStamps = 16;
 
@@ -153,6 +157,7 @@ struct FinTail {
     uint32_t* xerr;                      //   sticky timeout word, then the torn word (mapped host memory;
                                          //   read on the late path only)
     uint32_t* xstall;                    //   diagnostics (mppi_debug_peer_stall): a block's stall, null = none
+    uint32_t* xovl;                      // (V, A, ts) step counters for overlapped batches (MPPI_OVERLAP), null = off
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
@@ -178,24 +183,28 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // never pass for a later step's.  A block that gives a step up leaves the peers' words where they
 // are (a peer block on a rank that committed may still need them, below): the report alone tells
 // a peer still polling that step to give it up too.
-// All or nothing within a rank: the blocks of one step decide ONCE, per rank, whether the step
-// commits (every block updates its slice of u_prev) or is given up (every block keeps it).  Control
-// word kXDec + (step & 1) of the rank's own region holds the decision, (tag << 32) | kDecCommit or
-// kDecGiveUp, set by the first block's compare-and-swap (a block whose peers' words all arrived
-// proposes commit; a block that timed out or saw a report proposes give-up) and adopted by every
-// other block: a block that got its words on a rank that gave up holds its slice, and a block that
-// timed out on a rank that committed keeps polling its peers for a second bound (reports not heeded:
-// the peers' words stay in place) and completes.  Only if that second bound passes too is the rank's
-// warm start torn (that slice held, the others updated); the block then writes the step's tag into
-// the torn word next to the sticky word, and the resync takes its warm start from a rank that is
-// not torn.  Each step's first block clears the other parity's word (the previous step's: every
-// block of it has ended, the kernels of a queue run in order).
+// All or nothing within a rank: the blocks of one step either all update their slices of u_prev
+// or all keep them.  A block commits only when its peers' words all arrived within the bound AND
+// its final poll round saw no timeout report; it then marks control word kXDec + (step & 1) of the
+// rank's own region (tag << 32) | kDecCommit and updates its slice without waiting for anything.  A
+// late block (bound passed, or a report seen) reports first -- into every region, its own included,
+// so no block of its rank can commit after the report lands -- waits kDecGraceTicks (by then any
+// block whose final round came before the report has stored its mark: the store is issued right
+// after that round and lands within microseconds), and reads the word: if the rank committed, the
+// late block keeps polling its peers for a second bound (reports no longer heeded: the peers' words
+// stay in place) and completes; if not, the step is given up (every block of the rank is late or
+// holds).  Only if the second bound passes too is the rank's warm start torn (that slice kept, the
+// others updated): the block writes the step's tag into the torn word next to the sticky word, and
+// the resync takes its warm start from a rank that is not torn.  Each step's first block clears the
+// other parity's word (the previous step's: every block of it has ended, the kernels of a queue run
+// in order).
 constexpr int kMaxPeers = 8;
 constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
 constexpr int kXCtl = 16;        // control words at the head of a region (8 B each): kMaxPeers timeout
                                  // reports, then the two step parities' decision words
 constexpr int kXDec = kMaxPeers;
-constexpr uint32_t kDecCommit = 1u, kDecGiveUp = 2u;
+constexpr uint32_t kDecCommit = 1u;
+constexpr uint64_t kDecGraceTicks = 10000ull;   // 100 us (s_memrealtime, 100 MHz)
 constexpr int kVcStepWord = (int)(offsetof(VehicleConst, _pad) / 4) + 1;
 constexpr int kVcEpochWord = kVcStepWord + 1;
 constexpr uint32_t kTagValid = 0x80000000u;
@@ -249,6 +258,7 @@ struct FinParams {
     int32_t xn, xme;
     uint32_t* xerr;                      //   sticky timeout word, torn word (mapped host memory)
     uint32_t* xstall;                    //   diagnostics: a block's stall (mppi_debug_peer_stall), null = none
+    uint32_t* xovl;                      // step counters for overlapped batches (FinTail::xovl), null = off
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

@@ -25,6 +25,11 @@ namespace {
 // relative to the dispatch id -- step = arg + (dispatch id >> 1) -- so one argument block,
 // written once, serves every (rollout, finalize) pair the engine's queue runs
 constexpr int32_t kNoiseStepFromId = 0x100;
+// noise-mode flag of an overlapped native batch (MPPI_OVERLAP=1, mppi_step.cpp run_steps_aql): the
+// rollout is dispatched while the finalize before it still runs (no barrier bit), draws its first
+// group's normals, then waits for that finalize's blocks (DevParams::ovl counters) before it reads
+// u_prev or hands the vehicle constants on
+constexpr int32_t kNoiseOverlap = 0x200;
 __device__ __forceinline__ uint32_t step_of(uint32_t step_arg, int32_t noise_arg) {
     return (noise_arg & kNoiseStepFromId) ? step_arg + (uint32_t)(mppi_dispatch_id() >> 1) : step_arg;
 }

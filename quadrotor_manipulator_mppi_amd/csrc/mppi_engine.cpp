@@ -26,7 +26,7 @@ FinTail tail_of(const FinParams& f, int32_t mode) {
     t.out = f.out; t.u0 = f.u0; t.stats = f.stats; t.flags = f.flags; t.wraw = f.wraw; t.wsmooth = f.wsmooth;
     t.dst = f.dst; t.xbase = f.xbase; t.xslot = f.xslot; t.nslots = f.nslots; t.myslot = f.myslot; t.P = f.P;
     t.xpeers = f.xpeers; t.xlocal = f.xlocal; t.xn = f.xn; t.xme = f.xme; t.xerr = f.xerr;
-    t.xstall = f.xstall;
+    t.xstall = f.xstall; t.xovl = f.xovl;
     std::memcpy(t.sg, f.sg, sizeof(t.sg));
     return t;
 }
@@ -463,6 +463,19 @@ mppi_status mppi_create(const mppi_config* cfg, mppi_engine** out) {
     e->out_dbg = getenv("MPPI_DEBUG_OUT") ? atoi(getenv("MPPI_DEBUG_OUT")) : 0;
     if (const char* d = getenv("MPPI_DISPATCH")) e->aql_mode = !strcmp(d, "hip") ? 0 : !strcmp(d, "aql") ? 1 : 2;
     f.stamps = e->d_fstamps;
+    // experiment (MPPI_OVERLAP=1): overlapped native batches; k_rollout only (k_rollout_quad does not wait)
+    e->overlap = getenv("MPPI_OVERLAP") && atoi(getenv("MPPI_OVERLAP")) != 0 && c.model != MPPI_MODEL_QUADROTOR;
+    if (e->overlap) {
+        const size_t n = (size_t)e->V * e->A * e->fin_ts;
+        if (hipMalloc(&e->d_ovl, n * sizeof(uint32_t)) != hipSuccess || hipMemset(e->d_ovl, 0, n * sizeof(uint32_t)) != hipSuccess) {
+            fail(MPPI_ERR_HIP, "overlap counters");
+            mppi_destroy(e);
+            return MPPI_ERR_HIP;
+        }
+        f.xovl = e->d_ovl;
+        p.ovl = e->d_ovl;
+        p.ovl_n = e->A * e->fin_ts;
+    }
     {   // the finalize's tail parameters, one device copy per launch kind (constant for the
         // engine's life): the control step's FINAL, a shard's PACK, and FINAL into the device
         // scratch outputs (mppi_kernel_timing, probes)
@@ -522,7 +535,7 @@ void mppi_destroy(mppi_engine* e) {
     exchange_release(e);   // the communicator and the other ranks' mapped regions
     void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_xstall};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_xstall, e->d_ovl};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);

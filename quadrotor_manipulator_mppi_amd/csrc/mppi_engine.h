@@ -92,6 +92,9 @@ struct mppi_engine {
     uint32_t x_epoch = 0;               // the exchange epoch in the tags (mppi_dev.h peer_tag): moved by
                                         // mppi_set_step_counter and mppi_peer_reset on a connected engine
     uint32_t* d_xstall = nullptr;       // diagnostics (mppi_debug_peer_stall): a finalize block's stall
+    bool overlap = false;               // MPPI_OVERLAP=1 (experiment): native batches dispatch each rollout
+                                        // while the finalize before it runs (mppi_device.h kNoiseOverlap)
+    uint32_t* d_ovl = nullptr;          // its (V, A, fin_ts) step counters, one per finalize block
     mppi::VehicleConst* h_vc = nullptr; // pinned staging
     unsigned char* h_out = nullptr;     // pinned + mapped: k_finalize writes it directly
     unsigned char* h_out_dev = nullptr; // device view of h_out

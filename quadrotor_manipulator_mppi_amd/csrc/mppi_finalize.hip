@@ -149,6 +149,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     unsigned long long* const* xpeers = nullptr;   // peer exchange (null: off)
     unsigned long long xpl = 0ull;   // lane d < xn: rank d's region address (wave 0's stores read it by readlane)
     unsigned long long* xlocal = nullptr;
+    uint32_t* xovl = nullptr;   // overlapped batches' step counters (null: off)
     int32_t xn = 0, xme = 0;
     uint32_t xstep = 0u, xep = 0u;
     float sg[WIN > 0 ? WIN : 1];
@@ -159,7 +160,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
         wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
         up = T.u_prev; vcb = T.vc;
-        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme;
+        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme; xovl = T.xovl;
         if constexpr (WIN > 0) {
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
@@ -167,7 +168,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
                           "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
                           "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb), "+s"(xpeers), "+s"(xlocal), "+s"(xn),
-                          "+s"(xme));
+                          "+s"(xme), "+s"(xovl));
         if constexpr (WIN == 9)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
                               "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
@@ -396,32 +397,20 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         };
         bool late = poll(true), torn = false;
         if (mode == 0) {
-            // One decision per rank and step (mppi_dev.h kXDec): the first block's proposal, adopted
-            // by every block before any of them writes its slice of u_prev.
-            unsigned long long dec = 0ull;
-            if (lane == 0) {
-                gu64* dw = ctl + kXDec + par;
-                const unsigned long long mine = ((unsigned long long)tag << 32) | (late ? kDecGiveUp : kDecCommit);
-                unsigned long long cur = 0ull;
-                for (;;) {   // cur: the word as the swap found it
-                    if (__hip_atomic_compare_exchange_strong(dw, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT)) { dec = mine; break; }
-                    if ((uint32_t)(cur >> 32) == tag) { dec = cur; break; }   // decided by another block
-                    // (else an earlier step's word, left by a counter rewind: replace it)
-                }
-            }
-            const bool commit = ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dec) & 3u) == kDecCommit;
-            if (late && commit) {        // another block of this rank has updated its slice: complete
-                late = poll(false);      // (a second bound; the peers' words stay in place, reports aside)
-                torn = late;
-            } else if (!late && !commit) {
-                late = true;             // the rank gave the step up: keep this slice too
-            }
-            if (late && (torn || !commit)) {
-                // Give the step up on every rank: this rank's timeout report into every rank's region
-                // (its own included) -- a peer still polling this step gives it up at once -- and the
-                // sticky word the host reads (mppi_synchronize / mppi_read_outputs / mppi_peer_status);
-                // a torn rank also its torn word (the resync's source is a rank that is not torn).
+            // All or nothing within the rank (mppi_dev.h kXDec).  A block whose words all arrived in
+            // time with no report in sight marks the rank's decision word "commit" and goes on at
+            // once: nothing on this, the common, path waits.  A late block first reports (every
+            // region, this rank's own included: from then on no block of this rank can see its
+            // final round clean), then waits out kDecGraceTicks -- any block of this rank that found
+            // its words before the report arrived has marked its commit by then -- and reads the
+            // word: committed, it keeps polling its peers (a second bound, reports no longer heeded:
+            // the peers' words stay in place) and completes; otherwise the rank gives the step up.
+            gu64* dw = ctl + kXDec + par;
+            if (!late) {
+                if (lane == 0)
+                    __hip_atomic_store(dw, ((unsigned long long)tag << 32) | kDecCommit, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else {
                 const unsigned long long cw = ((unsigned long long)tag << 32) | 1ull;
 #pragma unroll
                 for (int d = 0; d < kMaxPeers; ++d) {
@@ -429,8 +418,18 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                     gst64* rg = region(d);
                     if (lane == 0) __hip_atomic_store(rg - kXCtl + xme, cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
-                uint32_t* xe = T.xerr;   // (read only here: the late path)
-                if (lane == 0 && xe) {
+                const uint64_t t_rep = __builtin_amdgcn_s_memrealtime();
+                while (__builtin_amdgcn_s_memrealtime() - t_rep < kDecGraceTicks) __builtin_amdgcn_s_sleep(8);
+                unsigned long long dec = 0ull;
+                if (lane == 0) dec = __hip_atomic_load(dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t dhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dec >> 32));
+                const uint32_t dlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dec);
+                if (dhi == tag && (dlo & 3u) == kDecCommit) {   // another block of this rank updated its slice
+                    late = poll(false);
+                    torn = late;
+                }
+                uint32_t* xe = T.xerr;   // (read only here: the late path) the sticky word the host reads
+                if (late && lane == 0 && xe) {   // (mppi_synchronize / mppi_read_outputs / mppi_peer_status)
                     __hip_atomic_store(xe, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if (torn) __hip_atomic_store(xe + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
@@ -590,6 +589,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     FSTAMP(6);
     FSTAMPRT(14);
     if (!(MPPI_FIN_KO & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this block's slice of u_prev is complete (the wait above): count the step for an overlapped
+    // rollout waiting on it (mppi_device.h kNoiseOverlap)
+    if (xovl != nullptr && mode == 0 && lane == 0)
+        __hip_atomic_fetch_add(xovl + ((size_t)v * A + a) * ts + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Native dispatch's check of its one assumption (mppi_aql.cpp step_create): the dispatch id the

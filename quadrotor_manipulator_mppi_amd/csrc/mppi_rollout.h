@@ -706,14 +706,19 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
     const float* usrc = u_prev + (size_t)v * HA;
     float ur[4];
     int jr[2];
-    {   // through a buffer resource over this vehicle's u_prev: 32-bit offsets, and the rows past
+    // an overlapped batch (kNoiseOverlap): u_prev is read only after the finalize before this
+    // rollout has written it (the wait below, after the first group's normals)
+    const bool ovl = (noise_arg & kNoiseOverlap) != 0;
+    auto load_u = [&]() __attribute__((always_inline)) {
+        // through a buffer resource over this vehicle's u_prev: 32-bit offsets, and the rows past
         // H*A read 0 from the range check (no per-load branch, no 64-bit address math)
         const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(usrc), 0, (MPPI_KO & 128) ? 0 : HA * 4, 0x00020000);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             ur[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(urs, (tid + j * nthr) * 4, 0, kAuxDev));
-    }
+    };
+    if (!ovl) load_u();
     if (MODEL != MPPI_MODEL_DRONE) {
         const int* js = (const int*)jtab;
 #pragma unroll
@@ -744,6 +749,21 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
             draw_normals<NA>(z0[c], kg, (uint32_t)(t0 + 64 * c), vkey, step_ctr, seed_lo, seed_hi);
+    }
+    if (ovl) {   // wave 0 waits until every finalize block of the previous step has counted it (its
+                 // slice of u_prev written and drained), then the block goes on together
+        if (wid == 0) {
+            const uint32_t* fl = pk.ovl + (size_t)v * pk.ovl_n;
+            const int nfl = pk.ovl_n;
+            for (;;) {
+                bool ok = true;
+                for (int i = lane; i < nfl; i += 64) ok &= (int32_t)(ld_dev(fl + i) - step_ctr) >= 0;
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        lds_barrier();
+        load_u();
     }
     SECTION("prologue_staging");
     STAMP(10);

@@ -359,6 +359,7 @@ static const char* aql_ineligible(const mppi_engine* e, bool batch = false) {
 // native dispatch it is relative to the dispatch id (kNoiseStepFromId in the noise-mode word).
 constexpr uint32_t kRollStepOff = 8;
 constexpr int32_t kNoiseStepFromId = 0x100;   // = mppi_device.h
+constexpr int32_t kNoiseOverlap = 0x200;      // = mppi_device.h
 
 // n steps as native AQL packets (mppi_aql.cpp).  *used = false: the caller runs them through
 // HIP (auto mode, native dispatch unavailable for this engine; e->aql_why says why).
@@ -401,6 +402,8 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
     p.vc0 = e->h_vc[0];
     p.step_ctr = 0u;                      // (set by step_prepare: relative to the dispatch id)
     p.noise_mode |= kNoiseStepFromId;
+    const bool ovl = e->overlap && n > 1;   // (experiment, MPPI_OVERLAP=1)
+    if (ovl) p.noise_mode |= kNoiseOverlap;
     FinParams f = e->fp;
     f.mode = 0;
     f.seq = 0u;   // completion: the batch's signal, not a flag
@@ -431,7 +434,13 @@ static mppi_status run_steps_aql(mppi_engine* e, int32_t n, bool* used) {
         e->aql_why = err;
         return e->aql_mode == 1 ? fail(MPPI_ERR_STATE, "native dispatch: %s", err.c_str()) : MPPI_OK;
     }
-    if (pr != 0 || mppi_aql::step_dispatch(e->aql, n, &err) != 0)
+    if (pr == 0 && ovl) {   // every finalize block's counter at the batch's first step (queue drained:
+                            // step_prepare above waited for it or found it idle)
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)e->d_ovl, (int)e->step_ctr, (size_t)e->V * e->A * e->fin_ts,
+                                  e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+    if (pr != 0 || mppi_aql::step_dispatch(e->aql, n, &err, ovl) != 0)
         return fail(MPPI_ERR_HIP, "native dispatch: %s", err.c_str());
     if (prof) {
         const auto c4 = now();

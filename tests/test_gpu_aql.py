@@ -257,3 +257,38 @@ def test_native_dispatch_refused_when_ids_are_not_packet_indices(monkeypatch):
     assert e.dispatch_info().endswith("calls: hip"), e.dispatch_info()
     e.close()
     ref.close()
+
+
+@pytest.mark.parametrize("model,kw", [("wholebody", dict(n_samples=8192, n_horizon=64)),
+                                      ("arm", dict(n_samples=4096, n_horizon=32, state_f64=True)),
+                                      ("wholebody", dict(n_samples=1024, n_horizon=64, n_vehicles=4))])
+def test_overlapped_batches_bit_identical(monkeypatch, model, kw):
+    """The overlapped native batch (experiment, MPPI_OVERLAP=1: every rollout after a batch's first
+    dispatched while the finalize before it runs, drawing its first group's normals and then waiting
+    on the finalize blocks' step counters before it reads u_prev) computes exactly what the HIP
+    launches compute: 3 batches of 40 steps, then a control call, u_prev / costs / outputs bit for bit."""
+    from quadrotor_manipulator_mppi_amd.engine import Engine, make_config
+    engines = []
+    for mode, ovl in (("hip", "0"), ("aql", "1")):
+        monkeypatch.setenv("MPPI_DISPATCH", mode)
+        monkeypatch.setenv("MPPI_OVERLAP", ovl)
+        e = Engine(make_config(model, device=0, seed=23, **kw))
+        for v in range(e.V):
+            e.set_target([0.1029, 0.4055, 1.6498], [-0.5, -0.5, 0.5, -0.5], vehicle=v)
+        e.set_state(_state(model, e.V))
+        engines.append(e)
+    monkeypatch.delenv("MPPI_DISPATCH")
+    monkeypatch.delenv("MPPI_OVERLAP")
+    h, a = engines
+    try:
+        for b in range(3):
+            for e in engines:
+                e.run_steps(40)
+            _same(h, a, f"overlapped batch {b}")
+        st = _state(model, h.V, shift=0.01)
+        for e in engines:
+            e.step(st)
+        _same(h, a, "control call after overlapped batches")
+    finally:
+        for e in engines:
+            e.close()
