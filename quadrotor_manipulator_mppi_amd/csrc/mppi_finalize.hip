@@ -150,6 +150,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     unsigned long long xpl = 0ull;   // lane d < xn: rank d's region address (wave 0's stores read it by readlane)
     unsigned long long* xlocal = nullptr;
     uint32_t* xovl = nullptr;   // overlapped batches' step counters (null: off)
+    uint32_t* xstall = nullptr;   // diagnostics (mppi_debug_peer_stall; null: off)
     int32_t xn = 0, xme = 0;
     uint32_t xstep = 0u, xep = 0u;
     float sg[WIN > 0 ? WIN : 1];
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
         wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
         up = T.u_prev; vcb = T.vc;
-        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme; xovl = T.xovl;
+        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme; xovl = T.xovl; xstall = T.xstall;
         if constexpr (WIN > 0) {
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
@@ -168,7 +169,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
                           "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
                           "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb), "+s"(xpeers), "+s"(xlocal), "+s"(xn),
-                          "+s"(xme), "+s"(xovl));
+                          "+s"(xme), "+s"(xovl), "+s"(xstall));
         if constexpr (WIN == 9)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
                               "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
@@ -321,7 +322,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         typedef __attribute__((address_space(1))) unsigned long long gu64;
         gu64* const ctl = (gu64*)xlocal - kXCtl;   // the ranks' timeout reports, the decision words
         if (mode == 0) {   // (this rank's own partial stays in registers: no round trip through memory)
-            if (uint32_t* xs = T.xstall) {   // diagnostics (mppi_debug_peer_stall): one block's stores late
+            if (uint32_t* xs = xstall) {   // diagnostics (mppi_debug_peer_stall): one block's stores late
                 const uint32_t sv = ld_dev(xs);
                 if (sv != 0u && (sv & 0xFFFFu) == (uint32_t)blk) {
                     const uint64_t t_s = __builtin_amdgcn_s_memrealtime(), ticks = (uint64_t)(sv >> 16) * 100000ull;

@@ -513,7 +513,8 @@ def test_peer_one_block_stalled_all_or_nothing(stall_ms):
     nothing (mppi_dev.h kXDec: one decision per rank and step, a compare-and-swap before any slice is
     written): rank 0's late block finds its rank committed and keeps polling for a second bound.
     3000 ms: the partial arrives within it -- both ranks end FULLY UPDATED, bit-identical to a pair
-    that never stalled, and no rank reports anything.  5000 ms: two bounds pass -- rank 0's warm start
+    that never stalled, no step given up (the late block's report still asks for a resync, which
+    follows).  5000 ms: two bounds pass -- rank 0's warm start
     is torn (that slice kept), which it reports (torn word, timeout report, nan flag 3) instead of
     leaving silently; rank 1 completes (its late block finds its rank committed, the words are in
     place) and is fully updated; the resync takes rank 1's warm start (the lowest rank not torn),
@@ -539,6 +540,8 @@ def test_peer_one_block_stalled_all_or_nothing(stall_ms):
         torn = [e.peer_info()[2] for e in pair]
         assert [e.peer_info()[1] for e in pair] == [0, 1]
         assert np.array_equal(u[1], want), "rank 1 fully updated"
+        # the late block reported the timeout either way (every region): the ranks resync before stepping on
+        assert all(any(e.peer_status()[1]) for e in pair), "the timeout is reported in every rank's region"
         if stall_ms < 4000:
             assert timed == [False, False] and torn == [0, 0], (timed, torn)
             assert np.array_equal(u[0], want), "rank 0 fully updated (its late block completed)"
@@ -550,18 +553,18 @@ def test_peer_one_block_stalled_all_or_nothing(stall_ms):
             exp = want.copy()
             exp[0, STALL_T, STALL_DIM] = held[0, STALL_T, STALL_DIM]
             assert np.array_equal(u[0], exp), "rank 0: exactly the stalled block's slice kept, reported torn"
-            # the resync (ShardedEngine.resync's choice, in process): the lowest rank that is not torn
-            src = min(r for r in range(2) if not torn[r])
-            assert src == 1
-            _sync_all(pair)
-            u_src, step = pair[src].get_u_prev(), pair[src].get_step_counter()
-            epoch = max(e.peer_status(reports=False)[2] for e in pair)
-            for e in pair:
-                e.peer_reset(step, epoch + 1)
-            for e in pair:
-                e.set_u_prev(u_src)
-            assert [e.peer_info()[2] for e in pair] == [0, 0]
-            assert all(np.array_equal(e.get_u_prev(), want) for e in pair), "whole warm starts after the resync"
+        # the resync (ShardedEngine.resync's choice, in process): the lowest rank that is not torn
+        src = min(r for r in range(2) if not torn[r])
+        assert src == (1 if stall_ms >= 4000 else 0)
+        _sync_all(pair)
+        u_src, step = pair[src].get_u_prev(), pair[src].get_step_counter()
+        epoch = max(e.peer_status(reports=False)[2] for e in pair)
+        for e in pair:
+            e.peer_reset(step, epoch + 1)
+        for e in pair:
+            e.set_u_prev(u_src)
+        assert [e.peer_info()[2] for e in pair] == [0, 0] and not any(any(e.peer_status()[1]) for e in pair)
+        assert all(np.array_equal(e.get_u_prev(), want) for e in pair), "whole warm starts after the resync"
         for p in (ref, pair):   # and stepping on: bit-identical to the pair that never stalled
             for e in p:
                 e.run_steps(5)
