@@ -158,6 +158,7 @@ struct FinTail {
                                          //   read on the late path only)
     uint32_t* xstall;                    //   diagnostics (mppi_debug_peer_stall): a block's stall, null = none
     uint32_t* xovl;                      // (V, A, ts) step counters for overlapped batches (MPPI_OVERLAP), null = off
+    unsigned long long* xdec;            // peer exchange: the rank's decision words, one per step parity
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
@@ -185,8 +186,10 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // a peer still polling that step to give it up too.
 // All or nothing within a rank: the blocks of one step either all update their slices of u_prev
 // or all keep them.  A block commits only when its peers' words all arrived within the bound AND
-// its final poll round saw no timeout report; it then marks control word kXDec + (step & 1) of the
-// rank's own region (tag << 32) | kDecCommit and updates its slice without waiting for anything.  A
+// its final poll round saw no timeout report; it then marks the rank's decision word for the step's
+// parity (FinTail::xdec: plain device memory, written and read at device scope like u_prev -- a
+// store into the uncached region would hold the block's final drain ~1 us longer) with
+// (tag << 32) | kDecCommit and updates its slice without waiting for anything.  A
 // late block (bound passed, or a report seen) reports first -- into every region, its own included,
 // so no block of its rank can commit after the report lands -- waits kDecGraceTicks (by then any
 // block whose final round came before the report has stored its mark: the store is issued right
@@ -200,9 +203,7 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // in order).
 constexpr int kMaxPeers = 8;
 constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
-constexpr int kXCtl = 16;        // control words at the head of a region (8 B each): kMaxPeers timeout
-                                 // reports, then the two step parities' decision words
-constexpr int kXDec = kMaxPeers;
+constexpr int kXCtl = 16;        // control words at the head of a region (8 B each; kMaxPeers timeout reports)
 constexpr uint32_t kDecCommit = 1u;
 constexpr uint64_t kDecGraceTicks = 10000ull;   // 100 us (s_memrealtime, 100 MHz)
 constexpr int kVcStepWord = (int)(offsetof(VehicleConst, _pad) / 4) + 1;
@@ -259,6 +260,7 @@ struct FinParams {
     uint32_t* xerr;                      //   sticky timeout word, torn word (mapped host memory)
     uint32_t* xstall;                    //   diagnostics: a block's stall (mppi_debug_peer_stall), null = none
     uint32_t* xovl;                      // step counters for overlapped batches (FinTail::xovl), null = off
+    unsigned long long* xdec;            // peer exchange: the rank's decision words (FinTail::xdec)
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

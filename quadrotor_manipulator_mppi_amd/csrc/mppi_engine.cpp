@@ -26,7 +26,7 @@ FinTail tail_of(const FinParams& f, int32_t mode) {
     t.out = f.out; t.u0 = f.u0; t.stats = f.stats; t.flags = f.flags; t.wraw = f.wraw; t.wsmooth = f.wsmooth;
     t.dst = f.dst; t.xbase = f.xbase; t.xslot = f.xslot; t.nslots = f.nslots; t.myslot = f.myslot; t.P = f.P;
     t.xpeers = f.xpeers; t.xlocal = f.xlocal; t.xn = f.xn; t.xme = f.xme; t.xerr = f.xerr;
-    t.xstall = f.xstall; t.xovl = f.xovl;
+    t.xstall = f.xstall; t.xovl = f.xovl; t.xdec = f.xdec;
     std::memcpy(t.sg, f.sg, sizeof(t.sg));
     return t;
 }
@@ -535,7 +535,7 @@ void mppi_destroy(mppi_engine* e) {
     exchange_release(e);   // the communicator and the other ranks' mapped regions
     void* dev[] = {e->d_xregion, e->d_xpeers, e->d_sigma, e->d_joints, e->d_vc, e->d_u_prev, e->d_noise_in, e->d_traj, e->d_noise_out,
                    e->d_S, e->d_hdr, e->d_rdata, e->d_out, e->d_wraw, e->d_wsmooth, e->d_w,
-                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_xstall, e->d_ovl};
+                   e->d_sinv, e->d_gamma, e->d_jtraj, e->d_xown, e->d_tail, e->d_stamps, e->d_fstamps, e->d_xstall, e->d_ovl, e->d_xdec};
     for (void* p : dev) if (p) (void)hipFree(p);
     if (e->h_out) (void)hipHostFree(e->h_out);
     if (e->h_vc) (void)hipHostFree(e->h_vc);

@@ -223,8 +223,12 @@ static mppi_status peer_bind(mppi_engine* e, std::vector<unsigned long long*> pt
     for (auto& p : ptrs) p += kXCtl;
     if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
     HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
+    if (!e->d_xdec) {
+        HIP_TRY(hipMalloc(&e->d_xdec, 2 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(e->d_xdec, 0, 2 * sizeof(unsigned long long)));
+    }
     FinParams& f = e->fp;
-    f.xpeers = e->d_xpeers; f.xlocal = xdata(e); f.xn = n; f.xme = me;
+    f.xpeers = e->d_xpeers; f.xlocal = xdata(e); f.xn = n; f.xme = me; f.xdec = e->d_xdec;
     FinTail t[2] = {tail_of(f, 0), tail_of(f, 2)};
     t[0].wraw = t[0].wsmooth = nullptr;   // (as at create: the step's FINAL stores no readback copies)
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -352,7 +356,7 @@ mppi_status mppi_peer_status(mppi_engine* e, uint32_t* sticky, uint64_t* reports
     return MPPI_OK;
 }
 
-// The connection as the kernel probe saw it and the torn word (mppi_dev.h kXDec): connected = the
+// The connection as the kernel probe saw it and the torn word (mppi_dev.h, "All or nothing within a rank"): connected = the
 // ranks whose tagged word reached this rank's region in mppi_peer_probe's phase 2 (0 before it).
 mppi_status mppi_peer_info(mppi_engine* e, int32_t* connected, int32_t* rank, uint32_t* torn) {
     if (!e) return fail(MPPI_ERR_INVALID_ARG, "null engine");
@@ -395,6 +399,7 @@ mppi_status mppi_peer_reset(mppi_engine* e, uint32_t step, uint32_t epoch) {
     if (use_device(e)) return MPPI_ERR_HIP;
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
+    if (e->d_xdec) HIP_TRY(hipMemset(e->d_xdec, 0, 2 * sizeof(unsigned long long)));
     HIP_TRY(hipDeviceSynchronize());
     *(volatile uint32_t*)(e->h_out + off_xerr(e)) = 0u;       // the sticky word
     *(volatile uint32_t*)(e->h_out + off_xerr(e) + 4) = 0u;   // the torn word

@@ -151,6 +151,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
     unsigned long long* xlocal = nullptr;
     uint32_t* xovl = nullptr;   // overlapped batches' step counters (null: off)
     uint32_t* xstall = nullptr;   // diagnostics (mppi_debug_peer_stall; null: off)
+    unsigned long long* xdec = nullptr;   // the rank's two decision words (peer exchange)
     int32_t xn = 0, xme = 0;
     uint32_t xstep = 0u, xep = 0u;
     float sg[WIN > 0 ? WIN : 1];
@@ -161,7 +162,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         mode = T.mode; model = T.model; qoff = T.qoff; nq = T.nq; sf64 = T.state_f64; odim = T.out_dim;
         wraw = T.wraw; wsmooth = T.wsmooth; u0p = T.u0; stats = T.stats; outp = T.out; flags = T.flags;
         up = T.u_prev; vcb = T.vc;
-        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme; xovl = T.xovl; xstall = T.xstall;
+        xpeers = T.xpeers; xlocal = T.xlocal; xn = T.xn; xme = T.xme; xovl = T.xovl; xstall = T.xstall; xdec = T.xdec;
         if constexpr (WIN > 0) {
 #pragma unroll
             for (int j = 0; j < WIN; ++j) sg[j] = T.sg[j];
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         asm volatile("" : "+s"(coef), "+s"(dt), "+s"(dt2), "+s"(mode), "+s"(model), "+s"(qoff), "+s"(nq),
                           "+s"(sf64), "+s"(odim), "+s"(wraw), "+s"(wsmooth), "+s"(u0p), "+s"(stats),
                           "+s"(outp), "+s"(flags), "+s"(up), "+s"(vcb), "+s"(xpeers), "+s"(xlocal), "+s"(xn),
-                          "+s"(xme), "+s"(xovl), "+s"(xstall));
+                          "+s"(xme), "+s"(xovl), "+s"(xstall), "+s"(xdec));
         if constexpr (WIN == 9)
             asm volatile("" : "+s"(sg[0]), "+s"(sg[1]), "+s"(sg[2]), "+s"(sg[3]), "+s"(sg[4]), "+s"(sg[5]),
                               "+s"(sg[6]), "+s"(sg[7]), "+s"(sg[8]));
@@ -330,8 +331,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                     if (lane == 0) __hip_atomic_store(xs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // once
                 }
             }
-            if (blk == 0 && lane == 0)   // the previous step's decision word (see mppi_dev.h kXDec)
-                __hip_atomic_store(ctl + kXDec + (par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blk == 0 && lane == 0)   // the previous step's decision word (mppi_dev.h, "All or nothing within a rank")
+                __hip_atomic_store((gu64*)xdec + (par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
             const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
 #pragma unroll
@@ -398,7 +399,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
         };
         bool late = poll(true), torn = false;
         if (mode == 0) {
-            // All or nothing within the rank (mppi_dev.h kXDec).  A block whose words all arrived in
+            // All or nothing within the rank (mppi_dev.h, "All or nothing within a rank").  A block whose words all arrived in
             // time with no report in sight marks the rank's decision word "commit" and goes on at
             // once: nothing on this, the common, path waits.  A late block first reports (every
             // region, this rank's own included: from then on no block of this rank can see its
@@ -406,7 +407,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             // its words before the report arrived has marked its commit by then -- and reads the
             // word: committed, it keeps polling its peers (a second bound, reports no longer heeded:
             // the peers' words stay in place) and completes; otherwise the rank gives the step up.
-            gu64* dw = ctl + kXDec + par;
+            gu64* dw = (gu64*)xdec + par;
             if (!late) {
                 if (lane == 0)
                     __hip_atomic_store(dw, ((unsigned long long)tag << 32) | kDecCommit, __ATOMIC_RELAXED,
