@@ -158,7 +158,7 @@ struct FinTail {
                                          //   read on the late path only)
     uint32_t* xstall;                    //   diagnostics (mppi_debug_peer_stall): a block's stall, null = none
     uint32_t* xovl;                      // (V, A, ts) step counters for overlapped batches (MPPI_OVERLAP), null = off
-    unsigned long long* xdec;            // peer exchange: the rank's decision words, one per step parity
+    unsigned long long* xdec;            // peer exchange: the rank's commit marks (2 parities x blocks)
     float sg[kMaxW];
 };
 // FINAL (the step's finalize), PACK (a shard's slot), SCRATCH (FINAL into device scratch outputs:
@@ -186,21 +186,20 @@ enum { kTailFinal = 0, kTailPack = 1, kTailScratch = 2, kTailReadback = 3, kTail
 // a peer still polling that step to give it up too.
 // All or nothing within a rank: the blocks of one step either all update their slices of u_prev
 // or all keep them.  A block commits only when its peers' words all arrived within the bound AND
-// its final poll round saw no timeout report; it then marks the rank's decision word for the step's
-// parity (FinTail::xdec: plain device memory, written and read at device scope like u_prev -- a
-// store into the uncached region would hold the block's final drain ~1 us longer) with
-// (tag << 32) | kDecCommit and updates its slice without waiting for anything.  A
+// its final poll round saw no timeout report; it then stores (tag << 32) | kDecCommit into its own
+// commit mark for the step's parity (FinTail::xdec: 2 x blocks words of plain device memory, written
+// and read at device scope like u_prev; one word per block, as 80 stores into one word serialise)
+// and updates its slice without waiting for anything.  A
 // late block (bound passed, or a report seen) reports first -- into every region, its own included,
 // so no block of its rank can commit after the report lands -- waits kDecGraceTicks (by then any
 // block whose final round came before the report has stored its mark: the store is issued right
-// after that round and lands within microseconds), and reads the word: if the rank committed, the
+// after that round and lands within microseconds), and reads the rank's marks: if one is this
+// step's (marks carry the tag, so earlier steps' never match), the
 // late block keeps polling its peers for a second bound (reports no longer heeded: the peers' words
 // stay in place) and completes; if not, the step is given up (every block of the rank is late or
 // holds).  Only if the second bound passes too is the rank's warm start torn (that slice kept, the
 // others updated): the block writes the step's tag into the torn word next to the sticky word, and
-// the resync takes its warm start from a rank that is not torn.  Each step's first block clears the
-// other parity's word (the previous step's: every block of it has ended, the kernels of a queue run
-// in order).
+// the resync takes its warm start from a rank that is not torn.
 constexpr int kMaxPeers = 8;
 constexpr int kXW = kHdr + 64;   // header + the widest window (CW <= 64)
 constexpr int kXCtl = 16;        // control words at the head of a region (8 B each; kMaxPeers timeout reports)
@@ -260,7 +259,7 @@ struct FinParams {
     uint32_t* xerr;                      //   sticky timeout word, torn word (mapped host memory)
     uint32_t* xstall;                    //   diagnostics: a block's stall (mppi_debug_peer_stall), null = none
     uint32_t* xovl;                      // step counters for overlapped batches (FinTail::xovl), null = off
-    unsigned long long* xdec;            // peer exchange: the rank's decision words (FinTail::xdec)
+    unsigned long long* xdec;            // peer exchange: the rank's commit marks (FinTail::xdec)
     float* u_prev;           // (V,H,A) in/out
     const VehicleConst* vc;  // (V); for V == 1 written by the rollout from its kernel arguments
     double* out;             // (V, out_dim)   -- mapped pinned host memory (zero-copy)

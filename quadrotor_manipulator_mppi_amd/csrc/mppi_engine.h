@@ -92,7 +92,7 @@ struct mppi_engine {
     uint32_t x_epoch = 0;               // the exchange epoch in the tags (mppi_dev.h peer_tag): moved by
                                         // mppi_set_step_counter and mppi_peer_reset on a connected engine
     uint32_t* d_xstall = nullptr;       // diagnostics (mppi_debug_peer_stall): a finalize block's stall
-    unsigned long long* d_xdec = nullptr;   // the peer exchange's decision words (2, one per step parity)
+    unsigned long long* d_xdec = nullptr;   // the peer exchange's commit marks (2 parities x finalize blocks)
     bool overlap = false;               // MPPI_OVERLAP=1 (experiment): native batches dispatch each rollout
                                         // while the finalize before it runs (mppi_device.h kNoiseOverlap)
     uint32_t* d_ovl = nullptr;          // its (V, A, fin_ts) step counters, one per finalize block

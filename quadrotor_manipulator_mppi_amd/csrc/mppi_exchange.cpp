@@ -224,8 +224,8 @@ static mppi_status peer_bind(mppi_engine* e, std::vector<unsigned long long*> pt
     if (!e->d_xpeers) HIP_TRY(hipMalloc(&e->d_xpeers, kMaxPeers * sizeof(void*)));
     HIP_TRY(hipMemcpy(e->d_xpeers, ptrs.data(), n * sizeof(void*), hipMemcpyHostToDevice));
     if (!e->d_xdec) {
-        HIP_TRY(hipMalloc(&e->d_xdec, 2 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(e->d_xdec, 0, 2 * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc(&e->d_xdec, 2 * fin_blocks(e) * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(e->d_xdec, 0, 2 * fin_blocks(e) * sizeof(unsigned long long)));
     }
     FinParams& f = e->fp;
     f.xpeers = e->d_xpeers; f.xlocal = xdata(e); f.xn = n; f.xme = me; f.xdec = e->d_xdec;
@@ -399,7 +399,7 @@ mppi_status mppi_peer_reset(mppi_engine* e, uint32_t step, uint32_t epoch) {
     if (use_device(e)) return MPPI_ERR_HIP;
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemset(e->d_xregion, 0, e->x_bytes));
-    if (e->d_xdec) HIP_TRY(hipMemset(e->d_xdec, 0, 2 * sizeof(unsigned long long)));
+    if (e->d_xdec) HIP_TRY(hipMemset(e->d_xdec, 0, 2 * fin_blocks(e) * sizeof(unsigned long long)));
     HIP_TRY(hipDeviceSynchronize());
     *(volatile uint32_t*)(e->h_out + off_xerr(e)) = 0u;       // the sticky word
     *(volatile uint32_t*)(e->h_out + off_xerr(e) + 4) = 0u;   // the torn word

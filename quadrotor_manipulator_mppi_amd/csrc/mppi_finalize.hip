@@ -31,6 +31,10 @@ constexpr int kMaxRec = 4096;
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
+// timing knockout for tools/ A/B experiments (results unsafe): 1 = no commit marks (peer exchange)
+#ifndef MPPI_FIN_NOMARK
+#define MPPI_FIN_NOMARK 0
+#endif
 // XCDs the finalize's blocks run on (8; 4 = the first four, see the block map in k_finalize)
 #ifndef MPPI_FIN_XCDS
 #define MPPI_FIN_XCDS 8
@@ -331,8 +335,6 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                     if (lane == 0) __hip_atomic_store(xs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // once
                 }
             }
-            if (blk == 0 && lane == 0)   // the previous step's decision word (mppi_dev.h, "All or nothing within a rank")
-                __hip_atomic_store((gu64*)xdec + (par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long wc = ((unsigned long long)tag << 32) | __float_as_uint(N);
             const unsigned long long wh = ((unsigned long long)tag << 32) | __float_as_uint(hown);
 #pragma unroll
@@ -407,10 +409,11 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             // its words before the report arrived has marked its commit by then -- and reads the
             // word: committed, it keeps polling its peers (a second bound, reports no longer heeded:
             // the peers' words stay in place) and completes; otherwise the rank gives the step up.
-            gu64* dw = (gu64*)xdec + par;
+            gu64* dw = (gu64*)xdec + par * nbk;   // this parity's marks, one word per block (no two blocks
+                                                  // store to one word: 80 stores into one would serialise)
             if (!late) {
-                if (lane == 0)
-                    __hip_atomic_store(dw, ((unsigned long long)tag << 32) | kDecCommit, __ATOMIC_RELAXED,
+                if (lane == 0 && !MPPI_FIN_NOMARK)
+                    __hip_atomic_store(dw + blk, ((unsigned long long)tag << 32) | kDecCommit, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 const unsigned long long cw = ((unsigned long long)tag << 32) | 1ull;
@@ -422,11 +425,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                 }
                 const uint64_t t_rep = __builtin_amdgcn_s_memrealtime();
                 while (__builtin_amdgcn_s_memrealtime() - t_rep < kDecGraceTicks) __builtin_amdgcn_s_sleep(8);
-                unsigned long long dec = 0ull;
-                if (lane == 0) dec = __hip_atomic_load(dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t dhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(dec >> 32));
-                const uint32_t dlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dec);
-                if (dhi == tag && (dlo & 3u) == kDecCommit) {   // another block of this rank updated its slice
+                bool marked = false;   // any block of this rank marked this step (the words carry the tag:
+                                       // an earlier step's marks never match)
+                for (size_t i = lane; i < nbk; i += 64) {
+                    const unsigned long long w = __hip_atomic_load(dw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    marked |= (uint32_t)(w >> 32) == tag && ((uint32_t)w & 3u) == kDecCommit;
+                }
+                if (__builtin_amdgcn_ballot_w64(marked) != 0ull) {   // another block of this rank updated its slice
                     late = poll(false);
                     torn = late;
                 }
