@@ -6,7 +6,7 @@
 #   scripts/gpu.sh prof     <tag> [workload ...]          rocprofv3 kernel traces of control steps only,
 #                                                         beside the unprofiled line of the same workload
 #   scripts/gpu.sh final    <tag>                         the round's evidence: tests, bench lines, rocprof of
-#                                                         the bench command, gloo and peer 2-rank rehearsals
+#                                                         the bench command, the plain `bench.py --gpus 2` rehearsal
 #                                                         (steps-only traces per workload: `prof`)
 #   scripts/gpu.sh ab       <tag> <lib.so[@ENV=v,..]> ..  same-process A/B of builds, native dispatch,
 #                                                         both library orders ([AB_REPS] [AB_RUNS])
@@ -14,6 +14,7 @@
 #   scripts/gpu.sh timeline <tag> <lib.so> <workload> ..  wall-clock step timelines (timeline build)
 #   scripts/gpu.sh probe    <tag> <probe> [args]          one tools/probes.py probe
 #   scripts/gpu.sh peer2    <tag>                         2-rank peer-exchange rehearsal of the N>1 bench path
+#   scripts/gpu.sh gpus2    <tag>                         `python bench.py --gpus 2` (bench.py starts the ranks)
 #   scripts/gpu.sh pmc      <tag> [bench.py args]         rocprofv3 counter passes, one group per pass
 #   scripts/gpu.sh traffic  <tag> [workload[:K] ...]      FETCH_SIZE / WRITE_SIZE per launch shape ->
 #                                                         gpurun_out/traffic_<tag>/pmc_rollout.json
@@ -39,7 +40,7 @@ fail() { echo "$1 rc=$2"; [ -f "$3" ] && tail -30 "$3"; exit $2; }
 run_tests() {   # $1 log, rest: files
   local log=$1; shift
   if [ $# -gt 0 ]; then timeout -k 10 600 $GPU_PYTEST -x "$@" > $log 2>&1
-  else timeout -k 10 600 $GPU_PYTEST -m gpu tests > $log 2>&1; fi
+  else MPPI_ACCURACY_OUT=$out/acc.json timeout -k 10 600 $GPU_PYTEST -m gpu tests > $log 2>&1; fi
   local rc=$?; echo "pytest rc=$rc"; tail -4 $log
   [ $rc -eq 0 ] || { grep -B5 -A40 "Error\|assert" $log | head -150; exit $rc; }
 }
@@ -85,6 +86,13 @@ peer2() {   # the N>1 bench path through the peer exchange, 2 ranks on this one 
   python3 -c "import json;d=json.load(open('$out/bench_peer2.json'));m=d['multi_gpu'];c=(d.get('secondary') or {}).get('c4') or {};print('peer2', d['config']['workload'], d['config']['parallelism'], 'step %.2f us'%(d['ms_per_step']*1e3), m['exchange'], m['native_comm_error'], '| c4', c.get('exchange'), ('step %.2f us'%(c.get('ms_per_step', 0)*1e3)) if c else None, '| fleet_c5', {k: f.get(k) for k in ('n_gpus', 'exchange', 'vehicles_per_gpu', 'vehicles_total', 'ms_per_step', 'value')} if (f := (d.get('secondary') or {}).get('fleet_c5')) else None)"
 }
 
+gpus2() {   # the N>1 bench line from ONE plain command: bench.py starts the 2 ranks itself (a child
+           # torch.distributed.run; 2 ranks on this one GPU: gloo process group, peer exchange)
+  timeout -k 10 600 python bench.py --gpus 2 --steps 50 --warmup 10 --latency-steps 20 > $out/bench_gpus2.json \
+      2> $out/bench_gpus2.err || fail "bench --gpus 2" $? $out/bench_gpus2.err
+  python3 -c "import json;d=json.load(open('$out/bench_gpus2.json'));m=d['multi_gpu'];print('gpus2 n_gpus', d['n_gpus'], m['exchange'], 'peer_ranks_connected', m['peer_ranks_connected'], m['process_group'], {k: (v.get('exchange'), v.get('rccl_nranks'), v.get('peer_ranks_connected'), (v.get('native_comm_error') or '')[:60]) for k, v in (d.get('secondary') or {}).items()})"
+}
+
 case $cmd in
 tests)
   run_tests $out/gpu_tests.log "$@" ;;
@@ -98,11 +106,10 @@ final)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $out/prof_bench -o run -- \
       python3 bench.py --steps 500 --warmup 50 --no-cpu-baseline --secondary "" --latency-steps 100 \
       > $out/prof_bench.json 2> $out/prof_bench.err || fail "rocprof bench" $? $out/prof_bench.err
-  MPPI_DIST_BACKEND=gloo MPPI_NATIVE_COMM=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
-      --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 50 --warmup 10 \
-      --latency-steps 20 > $out/bench_gloo2.json 2> $out/bench_gloo2.err || fail "gloo rehearsal" $? $out/bench_gloo2.err
-  peer2
+  gpus2
   echo "final done" ;;
+gpus2)
+  gpus2 ;;
 peer2)
   peer2 ;;
 ab)
