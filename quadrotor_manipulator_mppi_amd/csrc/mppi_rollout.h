@@ -63,6 +63,11 @@
 #ifndef MPPI_EPS_STASH
 #define MPPI_EPS_STASH 1
 #endif
+// experiment knob: after the block-combine barrier the waves with no record element (and
+// not wave 0, the header's) leave at once instead of computing the rescale factors too
+#ifndef MPPI_COMB_EXIT
+#define MPPI_COMB_EXIT 0
+#endif
 
 namespace {
 
@@ -1261,6 +1266,10 @@ __global__ void __launch_bounds__(512, (ONEG && !F64) ? 8 : (NCH >= 4 ? 2 : NCH 
             const int it = i / q, k0 = (blockIdx.x + it * p.nb) * nS;
             st_dev_run(Sv, (uint32_t)k0, s_stage + it * cost_run_stride(nS), min(nS, K - k0), i - it * q);
         }
+    }
+    if (MPPI_COMB_EXIT && wid != 0 && wid * 64 >= HA) {
+        drain_stores();
+        return;
     }
     // rho_b = the min of the 8 wave slots, which every thread reads for f_w anyway (an LDS
     // atomicMin before the barrier cost a waterfall loop and a ds_min per wave)
