@@ -537,7 +537,8 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
 #pragma clang fp contract(off)
         const float u0 = un;
         const float uold0 = u_old;
-        u0p[(size_t)v * A + a] = u0;
+        const bool plain = !(MPPI_FIN_KO & 256);   // (256: timing knockout, the plain host arrays not written)
+        if (plain) u0p[(size_t)v * A + a] = u0;
         double* out = outp + (size_t)v * odim;
         const bool drone_dim = (model == MPPI_MODEL_DRONE) || (model == MPPI_MODEL_WHOLEBODY && a < 3);
         double o1 = 0.0, o2 = 0.0;   // this dim's two outputs (position, velocity)
@@ -550,8 +551,10 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             const float vo = v0 + dt * u0;
             o1 = xo;
             o2 = vo;
-            out[a] = o1;
-            out[3 + a] = o2;
+            if (plain) {
+                out[a] = o1;
+                out[3 + a] = o2;
+            }
         } else {           // mppi.py:157-158 (qdes uses the OLD u_prev[0])
             const int j = a - qoff;
             const int base = (model == MPPI_MODEL_WHOLEBODY) ? 6 : 0;
@@ -565,11 +568,13 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
                 o1 = (double)((x0f + t1) + t2);
                 o2 = (double)(v0f + t3);
             }
-            out[base + j] = o1;
-            out[base + nq + j] = o2;
+            if (plain) {
+                out[base + j] = o1;
+                out[base + nq + j] = o2;
+            }
         }
         const float ess = (eta2 > 0.0f) ? eta * (eta / eta2) : 0.0f;
-        if (a == 0) {
+        if (plain && a == 0) {
             float* st = stats + (size_t)v * 4;
             st[0] = rho;
             st[1] = eta;
