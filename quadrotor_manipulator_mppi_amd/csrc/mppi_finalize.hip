@@ -27,7 +27,9 @@ constexpr int kFinThreads = 512;   // upper bound (LDS arrays are sized for 8 wa
 constexpr int kMaxRec = 4096;
 // timing knockouts for tools/ experiments (results wrong): 2 skips the mapped-memory
 // outputs, 8 exits after the wave fold, 16 exits at the start (the launch floor), 32 skips
-// the u_prev update, 64 skips the tail parameters' kernel-argument loads, 128 the final drain
+// the u_prev update, 128 the final drain, 256 the plain output arrays (the tagged records
+// stay).  (64, "tail parameters not loaded", was removed in round 6: since the tail moved to
+// FinTail its pointers are the only ones the stores use, and that build stored through null.)
 #ifndef MPPI_FIN_KO
 #define MPPI_FIN_KO 0
 #endif
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(NT) k_finalize(const float* __restrict__ hdr_b
             hd[i] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
             xv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(crsrc, (int)(coff + (uint32_t)(i * TR) * drs_b), 0, kAuxDev));
         }
-        if (base == 0 && !(MPPI_FIN_KO & 64)) {   // (64: timing knockout, tail parameters not loaded)
+        if (base == 0) {
             __builtin_amdgcn_sched_barrier(0);   // the first chunk's record loads issue first
             pin_tail();
         }
