@@ -384,6 +384,11 @@ def latency_at_rate(se, state, calls: int, period_s: float = 0.01, idle_s: float
     return lat
 
 
+class StepsGivenUp(RuntimeError):
+    """A peer-exchange step was given up during a measurement.  Every rank raises it at the same
+    point: the verdict comes from ShardedEngine.synchronize(), itself a collective."""
+
+
 def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1, lat_rate_calls=0):
     import torch
     from quadrotor_manipulator_mppi_amd.distributed import ShardedEngine
@@ -403,130 +408,132 @@ def run_workload(name, steps_n, warmup, world, dist, lat_steps, timing=True, bat
         # a rehearsal's gloo group carries the peer exchange's handle all-gather just as RCCL's would
         native = True
     se = ShardedEngine(seed=1234, native=native, mode=mode, **w)
-    eng = se.engine
-    V = eng.V   # this rank's vehicles (the fleet-wide ones: se.vehicles)
-    set_targets(eng, w["model"], se.vehicles)
-    if w["model"] == "quadrotor":   # warm start at hover thrust (quadrotor_mppi.MPPI does the same)
-        u = np.zeros((V, eng.H, eng.A), np.float32)
-        u[..., 0] = eng.cfg.quad_mass * eng.cfg.quad_gravity
-        eng.set_u_prev(u)
-    state = make_state(w["model"], se.vehicles.stop)[se.vehicles.start:]
-    eng.set_state(state)
-    red_dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else "cpu"
+    try:
+        eng = se.engine
+        V = eng.V   # this rank's vehicles (the fleet-wide ones: se.vehicles)
+        set_targets(eng, w["model"], se.vehicles)
+        if w["model"] == "quadrotor":   # warm start at hover thrust (quadrotor_mppi.MPPI does the same)
+            u = np.zeros((V, eng.H, eng.A), np.float32)
+            u[..., 0] = eng.cfg.quad_mass * eng.cfg.quad_gravity
+            eng.set_u_prev(u)
+        state = make_state(w["model"], se.vehicles.stop)[se.vehicles.start:]
+        eng.set_state(state)
+        red_dev = "cuda" if dist is not None and dist.get_backend() == "nccl" else "cpu"
 
-    def barrier():
-        # torch's synchronize first: it covers torch's own streams (idle here: the steps run on
-        # the engine's native queue or stream) and costs ~3 us of host time even on an idle
-        # device, which it now spends while the batch still runs; eng.synchronize() then waits
-        # for the batch's completion signal.  Both still bracket every batch.
-        torch.cuda.synchronize()
-        # on a multi-rank peer exchange se.synchronize() is itself a collective: the ranks agree that
-        # no step was given up (a MAX all-reduce, which doubles as the barrier); a timeout would have
-        # resynchronised the ranks and voids the measurement
-        if se.synchronize():
-            raise RuntimeError(f"{name}: a peer-exchange step timed out (ranks resynchronised): no valid timing")
-        if dist is not None:
-            if se.mode != "peer":
-                dist.barrier()
+        def barrier():
+            # torch's synchronize first: it covers torch's own streams (idle here: the steps run on
+            # the engine's native queue or stream) and costs ~3 us of host time even on an idle
+            # device, which it now spends while the batch still runs; eng.synchronize() then waits
+            # for the batch's completion signal.  Both still bracket every batch.
             torch.cuda.synchronize()
+            # on a multi-rank peer exchange se.synchronize() is itself a collective: the ranks agree that
+            # no step was given up (a MAX all-reduce, which doubles as the barrier); a timeout would have
+            # resynchronised the ranks and voids the measurement
+            if se.synchronize():
+                raise StepsGivenUp(f"{name}: a peer-exchange step timed out (ranks resynchronised): no valid timing")
+            if dist is not None:
+                if se.mode != "peer":
+                    dist.barrier()
+                torch.cuda.synchronize()
 
-    se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
-    barrier()
-    tim = None
-    if timing:   # per-kernel HIP-event timing in its own region, before the timed batches
-        n_t = max(200, steps_n // 5)
-        # n launches of each kernel back to back between one event pair, then n (rollout,
-        # finalize) pairs as a step runs them; median of 7 batches (a transient clock dip on
-        # the box moves one batch, not the median)
-        rs, fs, ps = zip(*[eng.kernel_timing_ex(n_t) for _ in range(7)])
-        r_us, f_us, p_us = float(np.median(rs)), float(np.median(fs)), float(np.median(ps))
-        tim = {"rollout_us": r_us, "finalize_us": f_us, "pair_us": p_us,
-               "rollout_in_step_us": max(r_us, p_us - f_us),
-               "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
-                         f"median of 7 batches, on the engine stream",
-               "rollout_us_batches": [round(x, 3) for x in rs]}
-        if se.mode == "rccl":   # the step's one collective alone (a collective call on every rank)
-            tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
-        se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
+        se.run_steps(warmup)   # one C call enqueues n steps (rollout -> all-reduce -> finalize when sharded)
         barrier()
-    # every batch follows its own W untimed warmup steps (the contract's warmup, repeated per
-    # batch): the host's launch rate after a pause is what a batch then measures less of
-    # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
-    prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
-    # GPU heat-up: the MI355X raises its clocks over ~10 ms of sustained load and drops them again
-    # when idle (profiles/r04/ramp: C3 9.93 us/step in a 20-step batch after 50 ms idle, 9.42
-    # after a 200-step burst, 9.02-9.05 after >= 1000 steps; consecutive 100-step chunks 9.33 ->
-    # 8.73 over the first ~10 ms).  So ahead of each batch's W warmup steps the steps run back to
-    # back for HEAT_MS first, and a batch measures the sustained rate, not the power-state ramp --
-    # at 20 steps (0.2 ms) it would otherwise time mostly the ramp.  The same step count on every
-    # rank (from the max-over-ranks step time), so peer-exchange ranks stay in lockstep.  The
-    # batches without the heat-up are reported too (timing.ms_per_step_batches_no_heatup).
-    heat_ms = float(os.environ.get("MPPI_BENCH_HEAT_MS", "15"))
-    n_heat = 0
-    if heat_ms > 0:
-        # the step's wall time from one timed 20-step batch (a host-paced step -- the torch
-        # collective's host round trip -- runs far longer than its kernel pair, and a heat-up sized
-        # from the pair ran ~0.3 s of such steps per batch), never below the kernel pair's time
-        barrier()
-        t0 = time.perf_counter()
-        se.run_steps(20)
-        barrier()
-        t_step = (time.perf_counter() - t0) / 20
-        if tim is not None:
-            t_step = max(t_step, tim["pair_us"] * 1e-6)
-        t_step = reduce_max([t_step], dist, red_dev)[0]
-        n_heat = int(min(20000, max(100, np.ceil(heat_ms * 1e-3 / t_step))))
-    bt_cold, _ = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
-    bt_cold = reduce_max(bt_cold, dist, red_dev)
-    heat_prime = prime
-    if n_heat:
-        heat_prime = (lambda: (se.run_steps(n_heat), se.run_steps(max(1, warmup)))) if prime is not None else \
-            (lambda: se.run_steps(n_heat))
-    bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, heat_prime)
-    bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
-    if tim is not None and dist is not None:   # the slowest rank's kernels
-        tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
-            [tim["rollout_us"], tim["rollout_in_step_us"]], dist, red_dev)
-    # host-inclusive control-call latency (set_state H2D + step + D2H outputs + check_reach)
-    lat = []
-    for i in range(lat_steps + 20 if lat_steps else 0):
-        t1 = time.perf_counter()
-        se.step(state)
-        if i >= 20:
-            lat.append(time.perf_counter() - t1)
-    eng.synchronize()
-    lat100 = latency_at_rate(se, state, lat_rate_calls) if lat_rate_calls else []
-    lat100p, pw_touches = [], 0
-    if lat_rate_calls:   # the same cadence with the engine's prewarm on (mppi_set_prewarm)
-        eng.set_prewarm(PREWARM_US)
-        lat100p = latency_at_rate(se, state, lat_rate_calls)
-        pw_touches = eng.prewarm()[1]
-        eng.set_prewarm(0)
-    if not lat and not lat100:
-        se.step(state)
-    dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
-    out, u0, st = eng.read_outputs()
-    if not os.environ.get("MPPI_FIN_DEBUG"):
-        assert np.isfinite(out).all(), "non-finite control output"
-    comm = eng.comm_info() if se.mode == "rccl" else None
-    # the peer exchange's own rank count: the ranks whose word reached this rank's region in the
-    # connection probe's kernel phase (mppi_peer_info), min over ranks
-    peer_n = None
-    if se.mode == "peer":
-        peer_n = int(-reduce_max([-float(eng.peer_info()[0])], dist, red_dev)[0])
-    res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
-           "lat100_prewarm": lat100p, "prewarm_touches": pw_touches,
-           "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
-           "K": eng.K, "H": eng.H,
-           "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
-           "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native, "exchange": se.mode,
-           "native_error": se.native_error, "world": world,
-           "backend": dist.get_backend() if dist is not None else None,
-           "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None,
-           "peer_ranks_connected": peer_n, "agree_every": se.agree_every if se.mode == "peer" and world > 1 else None,
-           "process_group": ({"backend": dist.get_backend(), "size": dist.get_world_size()} if dist is not None
-                             else None)}
-    eng.close()
+        tim = None
+        if timing:   # per-kernel HIP-event timing in its own region, before the timed batches
+            n_t = max(200, steps_n // 5)
+            # n launches of each kernel back to back between one event pair, then n (rollout,
+            # finalize) pairs as a step runs them; median of 7 batches (a transient clock dip on
+            # the box moves one batch, not the median)
+            rs, fs, ps = zip(*[eng.kernel_timing_ex(n_t) for _ in range(7)])
+            r_us, f_us, p_us = float(np.median(rs)), float(np.median(fs)), float(np.median(ps))
+            tim = {"rollout_us": r_us, "finalize_us": f_us, "pair_us": p_us,
+                   "rollout_in_step_us": max(r_us, p_us - f_us),
+                   "method": f"HIP events around {n_t} back-to-back launches (and {n_t} rollout+finalize pairs), "
+                             f"median of 7 batches, on the engine stream",
+                   "rollout_us_batches": [round(x, 3) for x in rs]}
+            if se.mode == "rccl":   # the step's one collective alone (a collective call on every rank)
+                tim["allreduce_us"] = float(np.median([eng.exchange_timing(n_t) for _ in range(3)]))
+            se.run_steps(max(1, warmup))   # back to the control loop (repacks the slots the timing summed)
+            barrier()
+        # every batch follows its own W untimed warmup steps (the contract's warmup, repeated per
+        # batch): the host's launch rate after a pause is what a batch then measures less of
+        # (profiles/r03/bench_prime_probe.txt: 20-step lines 11.1-11.3 us primed vs 11.0-12.8 not)
+        prime = None if os.environ.get("MPPI_BENCH_PRIME", "1") == "0" else (lambda: se.run_steps(max(1, warmup)))
+        # GPU heat-up: the MI355X raises its clocks over ~10 ms of sustained load and drops them again
+        # when idle (profiles/r04/ramp: C3 9.93 us/step in a 20-step batch after 50 ms idle, 9.42
+        # after a 200-step burst, 9.02-9.05 after >= 1000 steps; consecutive 100-step chunks 9.33 ->
+        # 8.73 over the first ~10 ms).  So ahead of each batch's W warmup steps the steps run back to
+        # back for HEAT_MS first, and a batch measures the sustained rate, not the power-state ramp --
+        # at 20 steps (0.2 ms) it would otherwise time mostly the ramp.  The same step count on every
+        # rank (from the max-over-ranks step time), so peer-exchange ranks stay in lockstep.  The
+        # batches without the heat-up are reported too (timing.ms_per_step_batches_no_heatup).
+        heat_ms = float(os.environ.get("MPPI_BENCH_HEAT_MS", "15"))
+        n_heat = 0
+        if heat_ms > 0:
+            # the step's wall time from one timed 20-step batch (a host-paced step -- the torch
+            # collective's host round trip -- runs far longer than its kernel pair, and a heat-up sized
+            # from the pair ran ~0.3 s of such steps per batch), never below the kernel pair's time
+            barrier()
+            t0 = time.perf_counter()
+            se.run_steps(20)
+            barrier()
+            t_step = (time.perf_counter() - t0) / 20
+            if tim is not None:
+                t_step = max(t_step, tim["pair_us"] * 1e-6)
+            t_step = reduce_max([t_step], dist, red_dev)[0]
+            n_heat = int(min(20000, max(100, np.ceil(heat_ms * 1e-3 / t_step))))
+        bt_cold, _ = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, prime)
+        bt_cold = reduce_max(bt_cold, dist, red_dev)
+        heat_prime = prime
+        if n_heat:
+            heat_prime = (lambda: (se.run_steps(n_heat), se.run_steps(max(1, warmup)))) if prime is not None else \
+                (lambda: se.run_steps(n_heat))
+        bt, benq = timed_batches(lambda: se.run_steps(steps_n), batches, barrier, heat_prime)
+        bt = reduce_max(bt, dist, red_dev)    # each batch: the slowest rank
+        if tim is not None and dist is not None:   # the slowest rank's kernels
+            tim["rollout_us_max_over_ranks"], tim["rollout_in_step_us_max_over_ranks"] = reduce_max(
+                [tim["rollout_us"], tim["rollout_in_step_us"]], dist, red_dev)
+        # host-inclusive control-call latency (set_state H2D + step + D2H outputs + check_reach)
+        lat = []
+        for i in range(lat_steps + 20 if lat_steps else 0):
+            t1 = time.perf_counter()
+            se.step(state)
+            if i >= 20:
+                lat.append(time.perf_counter() - t1)
+        eng.synchronize()
+        lat100 = latency_at_rate(se, state, lat_rate_calls) if lat_rate_calls else []
+        lat100p, pw_touches = [], 0
+        if lat_rate_calls:   # the same cadence with the engine's prewarm on (mppi_set_prewarm)
+            eng.set_prewarm(PREWARM_US)
+            lat100p = latency_at_rate(se, state, lat_rate_calls)
+            pw_touches = eng.prewarm()[1]
+            eng.set_prewarm(0)
+        if not lat and not lat100:
+            se.step(state)
+        dispatch = eng.dispatch_info()   # "<aql | hip: why not>; calls: <aql | hip>" (batches; control calls)
+        out, u0, st = eng.read_outputs()
+        if not os.environ.get("MPPI_FIN_DEBUG"):
+            assert np.isfinite(out).all(), "non-finite control output"
+        comm = eng.comm_info() if se.mode == "rccl" else None
+        # the peer exchange's own rank count: the ranks whose word reached this rank's region in the
+        # connection probe's kernel phase (mppi_peer_info), min over ranks
+        peer_n = None
+        if se.mode == "peer":
+            peer_n = int(-reduce_max([-float(eng.peer_info()[0])], dist, red_dev)[0])
+        res = {"batches_s": bt, "enqueue_s": benq, "batches_s_no_heatup": bt_cold, "heat_steps": n_heat, "lat100": lat100,
+               "lat100_prewarm": lat100p, "prewarm_touches": pw_touches,
+               "heat_ms": heat_ms, "dispatch": dispatch, "dt": float(np.median(bt)), "tim": tim, "lat": lat,
+               "K": eng.K, "H": eng.H,
+               "A": eng.A, "V": V, "strong": strong, "bytes": eng.rollout_bytes(), "ess": float(st[0].ess),
+               "model": w["model"], "state_f64": bool(eng.cfg.state_f64), "native": se.native, "exchange": se.mode,
+               "native_error": se.native_error, "world": world,
+               "backend": dist.get_backend() if dist is not None else None,
+               "rccl_nranks": comm[0] if comm else None, "rccl_rank": comm[1] if comm else None,
+               "peer_ranks_connected": peer_n, "agree_every": se.agree_every if se.mode == "peer" and world > 1 else None,
+               "process_group": ({"backend": dist.get_backend(), "size": dist.get_world_size()} if dist is not None
+                                 else None)}
+    finally:   # (also when a step is given up or a call raises: the next workload gets a clean device)
+        se.engine.close()
     return res
 
 
@@ -712,6 +719,39 @@ def secondary_entry(s, ns):
     return e
 
 
+def guarded(what: str, fn):
+    """One rank-local part of the line (N = 1 only: the drop-in latency, the CPU baseline, the
+    HBM fill): its failure becomes {"error": ...} in the line instead of costing the whole line."""
+    try:
+        return fn()
+    except Exception as ex:   # noqa: BLE001 -- reported in the line, never swallowed silently
+        log(f"{what} failed: {type(ex).__name__}: {ex}")
+        return {"error": f"{type(ex).__name__}: {ex}"}
+
+
+def run_secondaries(names, steps, world, dist, ranks_per_gpu, run=None):
+    """The secondary workloads, every rank in lockstep.  A failed secondary is reported in the line
+    as {"error": ...} and the next one runs: at N = 1 any exception (no collective to desynchronise);
+    at N > 1 only StepsGivenUp, which every rank raises at the same point (any other exception
+    ends the run, as a one-rank failure leaves the ranks' collectives unpaired)."""
+    run = run or run_workload
+    out = {}
+    for wname in names:
+        ns = max(50, steps // 5)
+        try:
+            s = run(wname, ns, 20, world, dist, 50, batches=3)
+        except Exception as ex:   # noqa: BLE001
+            if world > 1 and not isinstance(ex, StepsGivenUp):
+                raise
+            out[wname] = {"error": f"{type(ex).__name__}: {ex}"}
+            log(f"secondary {wname} failed: {out[wname]['error']}")
+            continue
+        s["ranks_per_gpu"] = ranks_per_gpu
+        out[wname] = secondary_entry(s, ns)
+        log(f"secondary {wname}: {out[wname]}")
+    return out
+
+
 def dropin_latency(n_calls):
     """The reference's own control call through the drop-in class (mppi_solver/mppi.py MPPI,
     the kinova node's tick: update_joint from the joint-state callback, then
@@ -818,27 +858,26 @@ def main():
     r = run_workload(workload, args.steps, args.warmup, world, dist, args.latency_steps,
                      timing=not args.no_kernel_timing, batches=batches, lat_rate_calls=args.latency_steps)
     r["ranks_per_gpu"] = ranks_per_gpu
-    secondary = {}
     extra = args.secondary if world == 1 else args.secondary_multi
+    secondary = {}
     if extra and r["tim"] is not None:
-        for wname in [s for s in extra.split(",") if s and s != workload]:
-            ns = max(50, args.steps // 5)
-            s = run_workload(wname, ns, 20, world, dist, 50, batches=3)   # (every rank, in lockstep)
-            s["ranks_per_gpu"] = ranks_per_gpu
-            secondary[wname] = secondary_entry(s, ns)
-            log(f"secondary {wname}: {secondary[wname]}")
+        secondary = run_secondaries([s for s in extra.split(",") if s and s != workload], args.steps, world, dist,
+                                    ranks_per_gpu)
     dropin = None
     if world == 1 and workload == "arm_c3" and args.latency_steps:
-        dropin = dropin_latency(args.latency_steps)
+        dropin = guarded("drop-in latency", lambda: dropin_latency(args.latency_steps))
         log(f"drop-in latency: {dropin}")
     cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, cpu_all = cpu_baseline(workload, args.cpu_budget)
+        cb = guarded("cpu baseline", lambda: cpu_baseline(workload, args.cpu_budget))
+        cpu, cpu_all = (cb, None) if isinstance(cb, dict) else cb   # (a dict: its error)
         log(f"cpu baseline: {cpu}")
     if rank == 0:
         measured = None
         if world == 1 and r["tim"] is not None:
-            measured = measured_hbm(local)
+            measured = guarded("measured HBM", lambda: measured_hbm(local))
+            if "error" in measured:
+                measured = None
             log(f"measured HBM: {measured}")
         line = make_line(workload, r, args, secondary, cpu, cpu_all, measured)
         line["host_binding"] = binding

@@ -214,3 +214,87 @@ def test_main_spawns_without_a_launcher(monkeypatch):
     monkeypatch.setenv("MPPI_BENCH_SPAWNED", "1")
     with pytest.raises(SystemExit, match="own launcher"):
         bench.main()
+
+
+# ------------------------------------------------------------ a failed secondary does not cost the line
+def test_secondary_failure_is_reported_not_fatal(monkeypatch):
+    """At N = 1 a secondary that raises (any exception) becomes {"error": ...} in the line and the
+    next secondary still runs; at N > 1 only StepsGivenUp (raised on every rank together) is
+    caught, anything else ends the run.  The engine is closed either way (run_workload's finally)."""
+    monkeypatch.setattr(bench, "log", lambda *a: None)
+    calls = []
+
+    def fake_run(name, ns, warmup, world, dist, lat_steps, batches=1):
+        calls.append(name)
+        if name == "bad":
+            raise RuntimeError("boom")
+        if name == "given_up":
+            raise bench.StepsGivenUp("given up")
+        r = _fake_result(world, 0, K=8192)
+        r["dt"] = float(np.median(r["batches_s"]))
+        return r
+
+    out = bench.run_secondaries(["bad", "good", "given_up"], 500, 1, None, 1, run=fake_run)
+    assert calls == ["bad", "good", "given_up"]
+    assert out["bad"] == {"error": "RuntimeError: boom"}
+    assert out["given_up"]["error"].startswith("StepsGivenUp")
+    assert out["good"]["value"] > 0 and out["good"]["samples"] == 8192
+    out = bench.run_secondaries(["given_up", "good"], 500, 2, None, 1, run=fake_run)
+    assert "error" in out["given_up"] and "value" in out["good"]
+    with pytest.raises(RuntimeError, match="boom"):
+        bench.run_secondaries(["bad"], 500, 2, None, 1, run=fake_run)
+
+
+def test_guarded_reports_the_error():
+    assert bench.guarded("x", lambda: 3) == 3
+    g = bench.guarded("x", lambda: 1 / 0)
+    assert g["error"].startswith("ZeroDivisionError")
+
+
+_MAIN_STUB = r"""
+import sys, numpy as np
+sys.path.insert(0, ROOT)
+sys.path.insert(0, TESTS)
+import bench
+from test_bench_cpu import _fake_result
+
+def fake_run(name, steps_n, warmup, world, dist, lat_steps, timing=True, batches=1, lat_rate_calls=0):
+    if name == "drone_c2":
+        raise RuntimeError("secondary boom")
+    r = _fake_result(1, 0, model="arm", K=4096, H=32)
+    r.update(A=7, strong=False, bytes=4096 * 32 * 76 + 4 * 4096, state_f64=True, exchange=None, native=False)
+    r["dt"] = float(np.median(r["batches_s"]))
+    return r
+
+def boom():
+    raise OSError("no host sampling here")
+
+bench.run_workload = fake_run
+bench.dropin_latency = lambda n: boom()
+bench.cpu_baseline = lambda w, b: boom()
+bench.measured_hbm = lambda local: {"fill_GBps": 5000.0}
+sys.argv = ["bench.py", "--steps", "20", "--warmup", "5", "--no-numa-bind", "--secondary", "drone_c2,wholebody_c4"]
+bench.main()
+"""
+
+
+def test_main_prints_one_line_when_parts_fail(tmp_path):
+    """bench.main() at N = 1 with a secondary, the drop-in latency and the CPU baseline all failing
+    (stand-ins for the GPU workloads, run in a child: main() re-points fd 1): still exactly one JSON
+    line on stdout, the failures named in it, the primary's numbers intact."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"ROOT = {os.path.dirname(here)!r}\nTESTS = {here!r}\n" + _MAIN_STUB
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(here))
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["config"]["workload"] == "arm_c3" and line["value"] > 0
+    assert line["secondary"]["drone_c2"] == {"error": "RuntimeError: secondary boom"}
+    assert line["secondary"]["wholebody_c4"]["value"] > 0
+    assert line["dropin_latency"]["error"].startswith("OSError")
+    assert line["cpu_baseline"]["error"].startswith("OSError") and line["cpu_baseline_all"] is None
+    assert line["roofline"]["peak_measured"] == {"fill_GBps": 5000.0}
