@@ -298,3 +298,79 @@ def test_main_prints_one_line_when_parts_fail(tmp_path):
     assert line["dropin_latency"]["error"].startswith("OSError")
     assert line["cpu_baseline"]["error"].startswith("OSError") and line["cpu_baseline_all"] is None
     assert line["roofline"]["peak_measured"] == {"fill_GBps": 5000.0}
+
+
+_RUN_STUB = r"""
+import sys, types, numpy as np
+sys.path.insert(0, ROOT)
+import torch
+torch.cuda.synchronize = lambda *a, **k: None   # (no device here: the fake engine below stands in)
+import bench
+import quadrotor_manipulator_mppi_amd.distributed as D
+
+class Stat:
+    ess = 123.0
+
+class FakeEngine:
+    def __init__(self, model, K, H, V):
+        self.K, self.H, self.V = K, H, V
+        self.A = {"arm": 7, "drone": 3, "wholebody": 10, "quadrotor": 4}[model]
+        self.cfg = types.SimpleNamespace(state_f64=model == "arm", quad_mass=1.0, quad_gravity=9.81)
+        self.closed = 0
+        self.steps = 0
+    def set_target(self, *a, **k): pass
+    def set_u_prev(self, u): pass
+    def set_state(self, s): assert s.shape[0] == self.V
+    def kernel_timing_ex(self, n): return (5.0, 4.0, 9.0)
+    def exchange_timing(self, n): return 2.0
+    def set_prewarm(self, us): pass
+    def prewarm(self): return (0, 7)
+    def dispatch_info(self): return "fake"
+    def read_outputs(self): return np.zeros((self.V, 14)), np.zeros((self.V, self.A)), [Stat()]
+    def comm_info(self): return (1, 0)
+    def peer_info(self): return (1, 0, 0)
+    def rollout_bytes(self): return self.K * self.H * 76
+    def synchronize(self): pass
+    def close(self):
+        self.closed += 1
+        CLOSED.append(self)
+
+CLOSED = []
+
+class FakeSharded:
+    def __init__(self, seed, native, mode, model, n_samples, n_horizon, n_vehicles=1, **kw):
+        self.engine = FakeEngine(model, n_samples, n_horizon, n_vehicles)
+        self.vehicles = range(0, n_vehicles)
+        self.mode, self.native, self.native_error, self.agree_every = mode or "torch", bool(native), None, None
+        self.give_up = FAIL == model
+    def run_steps(self, n): self.engine.steps += n
+    def synchronize(self): return self.give_up and self.engine.steps > 100
+    def step(self, state): return None
+
+D.ShardedEngine = FakeSharded
+r = bench.run_workload("arm_c3", 20, 5, 1, None, 3, batches=2, lat_rate_calls=2)
+assert r["K"] == 4096 and r["H"] == 32 and len(r["batches_s"]) == 2 and r["ess"] == 123.0, r
+assert r["tim"]["rollout_in_step_us"] == 5.0 and len(r["lat"]) == 3 and len(r["lat100"]) == 2
+assert [e.closed for e in CLOSED] == [1]
+FAIL = "wholebody"
+try:
+    bench.run_workload("wholebody_c4", 20, 5, 1, None, 0, batches=1)
+    raise SystemExit("no StepsGivenUp")
+except bench.StepsGivenUp:
+    pass
+assert [e.closed for e in CLOSED] == [1, 1], "the engine is closed when a step is given up"
+print("RUN_OK")
+"""
+
+
+def test_run_workload_with_a_stand_in_engine():
+    """run_workload's own logic on the CPU (the GPU engine replaced by a stand-in, torch.cuda's
+    synchronize stubbed): batches, kernel timing, latency legs and results; a given-up peer step
+    raises StepsGivenUp and the engine is still closed."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = f"ROOT = {os.path.dirname(here)!r}\nFAIL = None\n" + _RUN_STUB
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(here))
+    assert p.returncode == 0 and "RUN_OK" in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])
